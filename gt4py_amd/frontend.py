@@ -1,0 +1,777 @@
+"""GTScript frontend: Python AST of a stencil definition -> ``gt4py_amd.ir.Stencil``.
+
+A re-implementation (not a port) of the subset of the reference frontend that the
+hot path needs (``src/gt4py/cartesian/frontend/gtscript_frontend.py``:
+``GTScriptParser.run`` ``:2474-2549``, ``IRMaker`` ``:886``; ``defir_to_gtir.py:297``):
+
+- signature -> API fields (``Field[...]`` annotations) and scalar parameters,
+- ``with computation(ORDER), interval(...)`` blocks (also nested ``with interval`` sections),
+- assignments / aug-assignments to API fields and temporaries, ``if``/``elif``/``else``,
+  ``while``, ternaries, math builtins, casts, ``**`` and ``%`` (as NativeFunction POW/MOD,
+  ``defir_to_gtir.py:482-487``),
+- externals (``from __externals__ import X``) and compile-time ``if __INLINED(...)``,
+- inlining of ``@gtscript.function`` subroutines (single or tuple returns),
+- ``with horizontal(region[...])`` restrictions.
+
+Literal precision follows ``literal_int_precision``/``literal_float_precision``
+(``gtscript_frontend.py:913-990``).
+"""
+
+from __future__ import annotations
+
+import ast
+import builtins
+import inspect
+import itertools
+import numbers
+import textwrap
+import types
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from gt4py_amd import ir
+from gt4py_amd.ir import DataType
+
+_GTSCRIPT_FUNC_ATTR = "__gtscript_function__"
+
+
+class GTScriptSyntaxError(SyntaxError):
+    pass
+
+
+class GTScriptSymbolError(NameError):
+    pass
+
+
+class GTScriptDefinitionError(ValueError):
+    pass
+
+
+def annotate_function(func):
+    """Mark a ``@gtscript.function`` (parse lazily at inlining time)."""
+    if not isinstance(func, types.FunctionType):
+        raise TypeError(f"gtscript.function expects a function, got {func!r}")
+    setattr(func, _GTSCRIPT_FUNC_ATTR, True)
+    return func
+
+
+def is_gtscript_function(obj) -> bool:
+    return isinstance(obj, types.FunctionType) and getattr(obj, _GTSCRIPT_FUNC_ATTR, False)
+
+
+def _func_ast(func) -> ast.FunctionDef:
+    src = textwrap.dedent(inspect.getsource(func))
+    mod = ast.parse(src)
+    for node in mod.body:
+        if isinstance(node, ast.FunctionDef) and node.name == func.__name__:
+            return node
+    for node in ast.walk(mod):
+        if isinstance(node, ast.FunctionDef):
+            return node
+    raise GTScriptSyntaxError(f"Could not find the definition of {func.__name__}")
+
+
+def _func_namespace(func) -> Dict[str, Any]:
+    ns = dict(func.__globals__)
+    if func.__closure__:
+        for name, cell in zip(func.__code__.co_freevars, func.__closure__):
+            try:
+                ns[name] = cell.cell_contents
+            except ValueError:
+                pass
+    return ns
+
+
+def _scalar_dtype(annotation, options) -> DataType:
+    if annotation is float:
+        return DataType.FLOAT64 if options.literal_float_precision == 64 else DataType.FLOAT32
+    if annotation is int:
+        return DataType.INT64 if options.literal_int_precision == 64 else DataType.INT32
+    if annotation is bool:
+        return DataType.BOOL
+    try:
+        return DataType.from_np(np.dtype(annotation))
+    except TypeError as ex:
+        raise GTScriptDefinitionError(f"Invalid scalar parameter annotation {annotation!r}") from ex
+
+
+class _Scope:
+    """Name resolution for one function body (stencil or inlined gtscript.function)."""
+
+    def __init__(self, namespace: Dict[str, Any], externals: Dict[str, Any]):
+        self.namespace = namespace
+        self.externals = externals
+        self.imported: Dict[str, Any] = {}  # names imported from __externals__
+        self.aliases: Dict[str, Any] = {}  # function args -> ("field", name, offset) | ir.Expr
+        self.locals: Dict[str, str] = {}  # local (user) name -> temporary name
+
+    def lookup_external(self, name):
+        if name in self.imported:
+            return True, self.imported[name]
+        if name in self.namespace:
+            return True, self.namespace[name]
+        if hasattr(builtins, name):
+            return True, getattr(builtins, name)
+        return False, None
+
+
+class StencilParser:
+    def __init__(self, definition, externals: Dict[str, Any], options):
+        self.definition = definition
+        self.externals = dict(externals or {})
+        self.options = options
+        self.fields: Dict[str, ir.FieldDecl] = {}
+        self.scalars: Dict[str, ir.ScalarDecl] = {}
+        self.temporaries: Dict[str, ir.FieldDecl] = {}
+        self.temp_declared_dtype: Dict[str, DataType] = {}
+        self.api_order: List[str] = []
+        self._uid = itertools.count()
+        self.used_externals: Dict[str, Any] = {}
+
+    # ------------------------------------------------------------------ signature
+    def _parse_signature(self):
+        func = self.definition
+        sig = inspect.signature(func)
+        annotations = dict(getattr(func, "__annotations__", {}))
+        ns = _func_namespace(func)
+        from gt4py_amd.gtscript import _FieldDescriptor
+
+        for name, param in sig.parameters.items():
+            if param.kind in (param.VAR_POSITIONAL, param.VAR_KEYWORD):
+                raise GTScriptDefinitionError("Variable arguments are not supported in stencil definitions")
+            ann = annotations.get(name, param.annotation)
+            if isinstance(ann, str):
+                try:
+                    ann = eval(ann, ns)  # noqa: S307 - annotation strings from user code
+                except Exception as ex:
+                    raise GTScriptDefinitionError(f"Cannot resolve annotation {ann!r} of '{name}'") from ex
+            if ann is inspect.Parameter.empty:
+                raise GTScriptDefinitionError(f"Missing type annotation for argument '{name}'")
+            self.api_order.append(name)
+            if isinstance(ann, _FieldDescriptor):
+                if isinstance(ann.dtype, str):
+                    raise GTScriptDefinitionError(f"Unresolved dtype '{ann.dtype}' for field '{name}'")
+                axes = ann.axes_names
+                self.fields[name] = ir.FieldDecl(
+                    name=name,
+                    dtype=DataType.from_np(ann.dtype),
+                    axes=tuple(axes),
+                    data_dims=tuple(ann.data_dims),
+                )
+            else:
+                self.scalars[name] = ir.ScalarDecl(name=name, dtype=_scalar_dtype(ann, self.options))
+
+    # ------------------------------------------------------------------ helpers
+    def _new_temp_name(self, base: str) -> str:
+        return f"{base}__{next(self._uid)}"
+
+    def _literal(self, value) -> ir.Literal:
+        if isinstance(value, (bool, np.bool_)):
+            return ir.Literal(bool(value), DataType.BOOL)
+        if isinstance(value, np.generic):
+            return ir.Literal(value.item(), DataType.from_np(value.dtype))
+        if isinstance(value, numbers.Integral):
+            dt = DataType.INT64 if self.options.literal_int_precision == 64 else DataType.INT32
+            return ir.Literal(int(value), dt)
+        if isinstance(value, numbers.Real):
+            dt = DataType.FLOAT64 if self.options.literal_float_precision == 64 else DataType.FLOAT32
+            return ir.Literal(float(value), dt)
+        raise GTScriptSyntaxError(f"Unsupported literal {value!r}")
+
+    def _const_eval(self, node: ast.AST, scope: _Scope):
+        """Evaluate a compile-time expression (externals, literals, simple ops)."""
+        if isinstance(node, ast.Constant):
+            return node.value
+        if isinstance(node, ast.Name):
+            found, val = scope.lookup_external(node.id)
+            if not found:
+                raise GTScriptSymbolError(f"Unknown compile-time symbol '{node.id}'")
+            return val
+        if isinstance(node, ast.Attribute):
+            return getattr(self._const_eval(node.value, scope), node.attr)
+        if isinstance(node, ast.UnaryOp):
+            v = self._const_eval(node.operand, scope)
+            return {ast.USub: lambda x: -x, ast.UAdd: lambda x: +x, ast.Not: lambda x: not x}[type(node.op)](v)
+        if isinstance(node, ast.BoolOp):
+            vals = [self._const_eval(v, scope) for v in node.values]
+            if isinstance(node.op, ast.And):
+                return all(vals)
+            return any(vals)
+        if isinstance(node, ast.BinOp):
+            a, b = self._const_eval(node.left, scope), self._const_eval(node.right, scope)
+            ops = {
+                ast.Add: lambda x, y: x + y,
+                ast.Sub: lambda x, y: x - y,
+                ast.Mult: lambda x, y: x * y,
+                ast.Div: lambda x, y: x / y,
+                ast.FloorDiv: lambda x, y: x // y,
+                ast.Mod: lambda x, y: x % y,
+                ast.Pow: lambda x, y: x**y,
+            }
+            return ops[type(node.op)](a, b)
+        if isinstance(node, ast.Compare):
+            left = self._const_eval(node.left, scope)
+            res = True
+            for op, comp in zip(node.ops, node.comparators):
+                right = self._const_eval(comp, scope)
+                res = res and {
+                    ast.Eq: lambda x, y: x == y,
+                    ast.NotEq: lambda x, y: x != y,
+                    ast.Lt: lambda x, y: x < y,
+                    ast.LtE: lambda x, y: x <= y,
+                    ast.Gt: lambda x, y: x > y,
+                    ast.GtE: lambda x, y: x >= y,
+                    ast.Is: lambda x, y: x is y,
+                    ast.IsNot: lambda x, y: x is not y,
+                }[type(op)](left, right)
+                left = right
+            return res
+        if isinstance(node, ast.Tuple):
+            return tuple(self._const_eval(e, scope) for e in node.elts)
+        if isinstance(node, ast.Subscript):
+            return self._const_eval(node.value, scope)[self._const_eval(node.slice, scope)]
+        if isinstance(node, ast.Call):
+            fn = self._const_eval(node.func, scope)
+            args = [self._const_eval(a, scope) for a in node.args]
+            return fn(*args)
+        raise GTScriptSyntaxError(f"Not a compile-time expression: {ast.dump(node)}")
+
+    def _parse_import(self, stmt, scope: _Scope):
+        if isinstance(stmt, ast.ImportFrom) and stmt.module == "__externals__":
+            for alias in stmt.names:
+                if alias.name not in self.externals:
+                    raise GTScriptDefinitionError(f"Missing value for external symbol '{alias.name}'")
+                value = self.externals[alias.name]
+                scope.imported[alias.asname or alias.name] = value
+                self.used_externals[alias.name] = value
+        elif isinstance(stmt, ast.ImportFrom) and stmt.module in ("__gtscript__", "gt4py.cartesian.gtscript"):
+            return
+        elif isinstance(stmt, ast.ImportFrom) and stmt.module and stmt.module.endswith("gtscript"):
+            return
+        else:
+            raise GTScriptSyntaxError("Only 'from __externals__ import ...' and '__gtscript__' imports are allowed")
+
+    # ------------------------------------------------------------------ computations
+    def _call_name(self, node) -> Optional[str]:
+        if isinstance(node, ast.Call):
+            f = node.func
+            if isinstance(f, ast.Name):
+                return f.id
+            if isinstance(f, ast.Attribute):
+                return f.attr
+        return None
+
+    def _parse_order(self, node, scope) -> ir.LoopOrder:
+        if len(node.args) != 1:
+            raise GTScriptSyntaxError("computation() takes exactly one argument")
+        arg = node.args[0]
+        if isinstance(arg, ast.Name) and arg.id in ("PARALLEL", "FORWARD", "BACKWARD"):
+            return ir.LoopOrder[arg.id]
+        if isinstance(arg, ast.Attribute) and arg.attr in ("PARALLEL", "FORWARD", "BACKWARD"):
+            return ir.LoopOrder[arg.attr]
+        val = self._const_eval(arg, scope)
+        return ir.LoopOrder(int(val))
+
+    def _parse_interval(self, node, scope) -> ir.Interval:
+        args = node.args
+        if len(args) == 1 and isinstance(args[0], ast.Constant) and args[0].value is Ellipsis:
+            return ir.Interval(ir.AxisBound(ir.LevelMarker.START, 0), ir.AxisBound(ir.LevelMarker.END, 0))
+        if len(args) == 1:
+            # interval(k) == single level, or a slice-like K[...] expression
+            raise GTScriptSyntaxError("interval() needs (start, end) or ...")
+        if len(args) != 2:
+            raise GTScriptSyntaxError("interval() takes '...' or (start, end)")
+
+        def bound(a, is_start):
+            if isinstance(a, ast.Constant) and a.value is None:
+                return ir.AxisBound(ir.LevelMarker.START if is_start else ir.LevelMarker.END, 0)
+            v = self._const_eval(a, scope)
+            from gt4py_amd.gtscript import AxisIndex
+
+            if isinstance(v, AxisIndex):
+                level = ir.LevelMarker.START if v.index >= 0 else ir.LevelMarker.END
+                return ir.AxisBound(level, v.index + v.offset)
+            if v is None:
+                return ir.AxisBound(ir.LevelMarker.START if is_start else ir.LevelMarker.END, 0)
+            v = int(v)
+            if v < 0:
+                return ir.AxisBound(ir.LevelMarker.END, v)
+            if v == 0 and not is_start:
+                # interval(x, 0) is empty by python slicing semantics; keep START 0
+                return ir.AxisBound(ir.LevelMarker.START, 0)
+            return ir.AxisBound(ir.LevelMarker.START, v)
+
+        return ir.Interval(bound(args[0], True), bound(args[1], False))
+
+    def _parse_computation(self, stmt: ast.With, scope: _Scope) -> List[ir.VerticalLoop]:
+        items = stmt.items
+        first = items[0].context_expr
+        if self._call_name(first) != "computation":
+            raise GTScriptSyntaxError("Expected 'with computation(...)'")
+        order = self._parse_order(first, scope)
+        sections: List[ir.Section] = []
+        if len(items) == 2:
+            second = items[1].context_expr
+            if self._call_name(second) != "interval":
+                raise GTScriptSyntaxError("Expected 'interval(...)' after 'computation(...)'")
+            itv = self._parse_interval(second, scope)
+            sections.append(ir.Section(itv, self._parse_block(stmt.body, scope)))
+        elif len(items) == 1:
+            for sub in stmt.body:
+                if isinstance(sub, ast.Expr) and isinstance(sub.value, ast.Constant):
+                    continue
+                if not (isinstance(sub, ast.With) and self._call_name(sub.items[0].context_expr) == "interval"):
+                    raise GTScriptSyntaxError("Inside 'with computation(...)' only 'with interval(...)' blocks")
+                itv = self._parse_interval(sub.items[0].context_expr, scope)
+                sections.append(ir.Section(itv, self._parse_block(sub.body, scope)))
+        else:
+            raise GTScriptSyntaxError("Invalid 'with computation(...)' statement")
+
+        def key(sec):
+            b = sec.interval.start
+            return (0 if b.level == ir.LevelMarker.START else 1, b.offset)
+
+        sections.sort(key=key, reverse=(order == ir.LoopOrder.BACKWARD))
+        # drop empty sections (e.g. everything inlined away)
+        sections = [s for s in sections if s.body]
+        if not sections:
+            return []
+        return [ir.VerticalLoop(order, sections)]
+
+    # ------------------------------------------------------------------ statements
+    def _parse_block(self, stmts, scope: _Scope) -> List[ir.Stmt]:
+        out: List[ir.Stmt] = []
+        for s in stmts:
+            out.extend(self._parse_stmt(s, scope))
+        return out
+
+    def _is_inlined_call(self, node) -> bool:
+        return self._call_name(node) == "__INLINED"
+
+    def _parse_stmt(self, s, scope: _Scope) -> List[ir.Stmt]:
+        if isinstance(s, ast.Expr):
+            if isinstance(s.value, ast.Constant):
+                return []
+            if isinstance(s.value, ast.Call) and self._call_name(s.value) == "compile_assert":
+                if not self._const_eval(s.value.args[0], scope):
+                    raise GTScriptDefinitionError(f"compile_assert failed (line {s.lineno})")
+                return []
+            raise GTScriptSyntaxError(f"Invalid expression statement (line {s.lineno})")
+        if isinstance(s, ast.Pass):
+            return []
+        if isinstance(s, (ast.Import, ast.ImportFrom)):
+            self._parse_import(s, scope)
+            return []
+        if isinstance(s, ast.Assign):
+            if len(s.targets) != 1:
+                raise GTScriptSyntaxError("Chained assignments are not supported")
+            return self._parse_assign(s.targets[0], s.value, scope)
+        if isinstance(s, ast.AnnAssign):
+            if s.value is None:
+                raise GTScriptSyntaxError("Annotated declaration without value")
+            ann = self._const_eval(s.annotation, scope)
+            if isinstance(s.target, ast.Name):
+                tname = self._temp_for_local(s.target.id, scope, create=True)
+                self.temp_declared_dtype[tname] = _scalar_dtype(ann, self.options)
+            return self._parse_assign(s.target, s.value, scope)
+        if isinstance(s, ast.AugAssign):
+            binop = ast.BinOp(left=_load_copy(s.target), op=s.op, right=s.value)
+            ast.copy_location(binop, s)
+            return self._parse_assign(s.target, binop, scope)
+        if isinstance(s, ast.If):
+            if self._is_inlined_call(s.test):
+                cond = self._const_eval(s.test.args[0], scope)
+                return self._parse_block(s.body if cond else s.orelse, scope)
+            pre: List[ir.Stmt] = []
+            cond = self._parse_expr(s.test, scope, pre)
+            body = self._parse_block(s.body, scope)
+            orelse = self._parse_block(s.orelse, scope)
+            return pre + [ir.If(cond, body, orelse)]
+        if isinstance(s, ast.While):
+            pre = []
+            cond = self._parse_expr(s.test, scope, pre)
+            if pre:
+                raise GTScriptSyntaxError("Function calls in while conditions are not supported")
+            return [ir.While(cond, self._parse_block(s.body, scope))]
+        if isinstance(s, ast.With):
+            name = self._call_name(s.items[0].context_expr)
+            if name == "horizontal":
+                masks = []
+                for item in s.items:
+                    for reg in item.context_expr.args:
+                        masks.append(self._parse_region(reg, scope))
+                return [ir.HorizontalRegion(masks, self._parse_block(s.body, scope))]
+            raise GTScriptSyntaxError(f"Invalid 'with' statement inside a computation (line {s.lineno})")
+        if isinstance(s, ast.Return):
+            raise GTScriptSyntaxError("'return' is only allowed in gtscript functions")
+        raise GTScriptSyntaxError(f"Unsupported statement {type(s).__name__} (line {getattr(s, 'lineno', '?')})")
+
+    def _parse_region(self, node, scope) -> ir.HorizontalMask:
+        # region[I[0]:I[0]+2, J[-1]-2:J[-1]]
+        if not (isinstance(node, ast.Subscript)):
+            raise GTScriptSyntaxError("Expected region[...]")
+        sl = node.slice
+        elts = sl.elts if isinstance(sl, ast.Tuple) else [sl]
+        if len(elts) != 2:
+            raise GTScriptSyntaxError("region[...] needs an I and a J slice")
+        from gt4py_amd.gtscript import AxisIndex
+
+        def bound(expr):
+            if expr is None:
+                return None
+            v = self._const_eval(expr, scope)
+            if isinstance(v, AxisIndex):
+                level = ir.LevelMarker.START if v.index >= 0 else ir.LevelMarker.END
+                return ir.AxisBound(level, v.index + v.offset)
+            if isinstance(v, int):
+                return ir.AxisBound(ir.LevelMarker.END if v < 0 else ir.LevelMarker.START, v)
+            raise GTScriptSyntaxError("Region bounds must be axis indices like I[0] + n")
+
+        res = []
+        for e in elts:
+            if isinstance(e, ast.Slice):
+                res.append(ir.HorizontalInterval(bound(e.lower), bound(e.upper)))
+            else:
+                b = bound(e)
+                res.append(ir.HorizontalInterval(b, ir.AxisBound(b.level, b.offset + 1)))
+        return ir.HorizontalMask(res[0], res[1])
+
+    def _temp_for_local(self, name: str, scope: _Scope, create: bool) -> Optional[str]:
+        if name in scope.locals:
+            return scope.locals[name]
+        if not create:
+            return None
+        # stencil-level names keep their name, function locals get a unique suffix
+        tname = name if scope is self._root_scope else self._new_temp_name(name)
+        if tname in self.fields or tname in self.scalars:
+            raise GTScriptDefinitionError(f"Cannot assign to parameter '{name}'")
+        scope.locals[name] = tname
+        return tname
+
+    def _parse_assign(self, target, value, scope: _Scope) -> List[ir.Stmt]:
+        pre: List[ir.Stmt] = []
+        if isinstance(target, ast.Tuple):
+            if not isinstance(value, ast.Call):
+                raise GTScriptSyntaxError("Tuple assignment requires a gtscript function call")
+            results = self._inline_call(value, scope, pre, n_results=len(target.elts))
+            out = pre
+            for t, r in zip(target.elts, results):
+                out.extend(self._assign_to(t, r, scope))
+            return out
+        val = self._parse_expr(value, scope, pre)
+        return pre + self._assign_to(target, val, scope)
+
+    def _assign_to(self, target, val: ir.Expr, scope: _Scope) -> List[ir.Stmt]:
+        if isinstance(target, ast.Subscript):
+            base = target.value
+            if not isinstance(base, ast.Name):
+                raise GTScriptSyntaxError("Invalid assignment target")
+            offs = self._parse_offset(target.slice, scope)
+            if any(offs):
+                raise GTScriptSyntaxError(f"Assignment to '{base.id}' with non-zero offset {offs}")
+            target = base
+        if not isinstance(target, ast.Name):
+            raise GTScriptSyntaxError("Invalid assignment target")
+        name = target.id
+        if name in scope.aliases:
+            alias = scope.aliases[name]
+            if isinstance(alias, tuple) and alias[0] == "field" and alias[2] == (0, 0, 0):
+                name_res = alias[1]
+            else:
+                raise GTScriptSyntaxError(f"Cannot assign to function argument '{name}'")
+        elif name in self.fields and scope is self._root_scope:
+            name_res = name
+        elif name in self.scalars and scope is self._root_scope:
+            raise GTScriptDefinitionError(f"Cannot assign to scalar parameter '{name}'")
+        else:
+            name_res = self._temp_for_local(name, scope, create=True)
+            if name_res not in self.temporaries:
+                self.temporaries[name_res] = ir.FieldDecl(name_res, DataType.AUTO, is_temporary=True)
+        return [ir.Assign(ir.FieldAccess(name_res, (0, 0, 0)), val)]
+
+    # ------------------------------------------------------------------ expressions
+    def _parse_offset(self, sl, scope) -> Tuple[int, int, int]:
+        elts = sl.elts if isinstance(sl, ast.Tuple) else [sl]
+        vals = [int(self._const_eval(e, scope)) for e in elts]
+        return tuple(vals)
+
+    def _field_access(self, name: str, offset, scope) -> ir.FieldAccess:
+        decl = self.fields.get(name) or self.temporaries.get(name)
+        off = list(offset)
+        if decl is not None and name in self.fields:
+            mask = decl.mask
+            if len(off) == sum(mask) and len(off) != 3:
+                it = iter(off)
+                off = [next(it) if m else 0 for m in mask]
+        if len(off) != 3:
+            raise GTScriptSyntaxError(f"Invalid offset {tuple(offset)} for '{name}'")
+        return ir.FieldAccess(name, tuple(off))
+
+    def _resolve_name(self, name: str, scope: _Scope, offset=(0, 0, 0)) -> ir.Expr:
+        if name in scope.aliases:
+            alias = scope.aliases[name]
+            if isinstance(alias, tuple) and alias[0] == "field":
+                base_off = alias[2]
+                return self._field_access(alias[1], tuple(a + b for a, b in zip(base_off, offset)), scope)
+            if any(offset):
+                raise GTScriptSyntaxError(f"Offset access to non-field argument '{name}'")
+            return alias
+        if name in scope.locals:
+            return ir.FieldAccess(scope.locals[name], tuple(offset))
+        if scope is self._root_scope:
+            if name in self.fields:
+                return self._field_access(name, offset, scope)
+            if name in self.scalars:
+                if any(offset):
+                    raise GTScriptSyntaxError(f"Offset access to scalar '{name}'")
+                return ir.ScalarAccess(name)
+        if name in ("True", "False"):
+            return ir.Literal(name == "True", DataType.BOOL)
+        found, val = scope.lookup_external(name)
+        if found:
+            if isinstance(val, (bool, np.bool_, numbers.Number, np.generic)):
+                if any(offset):
+                    raise GTScriptSyntaxError(f"Offset access to constant '{name}'")
+                self.used_externals.setdefault(name, val)
+                return self._literal(val)
+        raise GTScriptSymbolError(f"Unknown symbol '{name}'")
+
+    def _parse_expr(self, node, scope: _Scope, pre: List[ir.Stmt]) -> ir.Expr:
+        if isinstance(node, ast.Constant):
+            if node.value is None:
+                raise GTScriptSyntaxError("None is not a valid expression")
+            return self._literal(node.value)
+        if isinstance(node, ast.Name):
+            return self._resolve_name(node.id, scope)
+        if isinstance(node, ast.Subscript):
+            if isinstance(node.value, ast.Name):
+                offs = self._parse_offset(node.slice, scope)
+                return self._resolve_name(node.value.id, scope, offs)
+            if isinstance(node.value, ast.Subscript):
+                raise GTScriptSyntaxError("Data-dimension indexing is not supported yet")
+            raise GTScriptSyntaxError("Invalid subscript")
+        if isinstance(node, ast.Attribute):
+            v = self._const_eval(node, scope)
+            return self._literal(v)
+        if isinstance(node, ast.UnaryOp):
+            operand = self._parse_expr(node.operand, scope, pre)
+            op = {ast.USub: "-", ast.UAdd: "+", ast.Not: "not"}.get(type(node.op))
+            if op is None:
+                raise GTScriptSyntaxError(f"Unsupported unary operator {type(node.op).__name__}")
+            return ir.UnaryOp(op, operand)
+        if isinstance(node, ast.BinOp):
+            left = self._parse_expr(node.left, scope, pre)
+            right = self._parse_expr(node.right, scope, pre)
+            if isinstance(node.op, ast.Pow):
+                return ir.NativeCall("pow", [left, right])
+            if isinstance(node.op, ast.Mod):
+                return ir.NativeCall("mod", [left, right])
+            op = {ast.Add: "+", ast.Sub: "-", ast.Mult: "*", ast.Div: "/"}.get(type(node.op))
+            if op is None:
+                raise GTScriptSyntaxError(f"Unsupported binary operator {type(node.op).__name__}")
+            return ir.BinaryOp(op, left, right)
+        if isinstance(node, ast.BoolOp):
+            op = "and" if isinstance(node.op, ast.And) else "or"
+            vals = [self._parse_expr(v, scope, pre) for v in node.values]
+            res = vals[0]
+            for v in vals[1:]:
+                res = ir.BinaryOp(op, res, v)
+            return res
+        if isinstance(node, ast.Compare):
+            ops = {ast.Gt: ">", ast.Lt: "<", ast.GtE: ">=", ast.LtE: "<=", ast.Eq: "==", ast.NotEq: "!="}
+            left = self._parse_expr(node.left, scope, pre)
+            res = None
+            for op, comp in zip(node.ops, node.comparators):
+                right = self._parse_expr(comp, scope, pre)
+                if type(op) not in ops:
+                    raise GTScriptSyntaxError(f"Unsupported comparison {type(op).__name__}")
+                c = ir.BinaryOp(ops[type(op)], left, right)
+                res = c if res is None else ir.BinaryOp("and", res, c)
+                left = right
+            return res
+        if isinstance(node, ast.IfExp):
+            cond = self._parse_expr(node.test, scope, pre)
+            t = self._parse_expr(node.body, scope, pre)
+            f = self._parse_expr(node.orelse, scope, pre)
+            return ir.TernaryOp(cond, t, f)
+        if isinstance(node, ast.Call):
+            return self._parse_call(node, scope, pre)
+        raise GTScriptSyntaxError(f"Unsupported expression {type(node).__name__}")
+
+    def _parse_call(self, node: ast.Call, scope: _Scope, pre) -> ir.Expr:
+        fname = self._call_name(node)
+        func_obj = None
+        if isinstance(node.func, ast.Name):
+            if node.func.id in scope.aliases or node.func.id in scope.locals:
+                raise GTScriptSyntaxError(f"'{node.func.id}' is not callable")
+            found, func_obj = scope.lookup_external(node.func.id)
+            if not found:
+                raise GTScriptSymbolError(f"Unknown function '{node.func.id}'")
+        elif isinstance(node.func, ast.Attribute):
+            func_obj = self._const_eval(node.func, scope)
+        if is_gtscript_function(func_obj):
+            (res,) = self._inline_call(node, scope, pre, n_results=1, func=func_obj)
+            return res
+        native = None
+        builtin_name = getattr(func_obj, "_gtscript_builtin_", None)
+        if builtin_name is not None:
+            native = builtin_name
+        elif func_obj in (builtins.abs, builtins.min, builtins.max, builtins.round):
+            native = {builtins.abs: "abs", builtins.min: "min", builtins.max: "max", builtins.round: "round"}[func_obj]
+        elif func_obj in (np.int32, np.int64, np.float32, np.float64, builtins.float, builtins.int):
+            if func_obj is builtins.float:
+                native = "float64" if self.options.literal_float_precision == 64 else "float32"
+            elif func_obj is builtins.int:
+                native = "int64" if self.options.literal_int_precision == 64 else "int32"
+            else:
+                native = np.dtype(func_obj).name
+        elif fname in ir.NATIVE_FUNCTIONS:
+            native = fname
+        if native is None:
+            raise GTScriptSyntaxError(f"Unsupported function call '{fname}'")
+        if node.keywords:
+            raise GTScriptSyntaxError(f"Keyword arguments are not supported for '{fname}'")
+        args = [self._parse_expr(a, scope, pre) for a in node.args]
+        if len(args) != ir.NATIVE_FUNCTIONS[native]:
+            raise GTScriptSyntaxError(f"{native} accepts {ir.NATIVE_FUNCTIONS[native]} arguments, {len(args)} given")
+        return ir.NativeCall(native, args)
+
+    # ------------------------------------------------------------------ inlining
+    def _inline_call(self, node: ast.Call, scope: _Scope, pre: List[ir.Stmt], n_results: int, func=None):
+        if func is None:
+            if isinstance(node.func, ast.Name):
+                found, func = scope.lookup_external(node.func.id)
+                if not found:
+                    raise GTScriptSymbolError(f"Unknown function '{node.func.id}'")
+            else:
+                func = self._const_eval(node.func, scope)
+        if not is_gtscript_function(func):
+            raise GTScriptSyntaxError(f"'{getattr(func, '__name__', func)}' is not a gtscript function")
+        fdef = _func_ast(func)
+        sig = inspect.signature(func)
+        # bind arguments
+        bound_args: Dict[str, ast.AST] = {}
+        names = list(sig.parameters)
+        for i, a in enumerate(node.args):
+            bound_args[names[i]] = a
+        for kw in node.keywords:
+            bound_args[kw.arg] = kw.value
+        for pname, p in sig.parameters.items():
+            if pname not in bound_args:
+                if p.default is inspect.Parameter.empty:
+                    raise GTScriptSyntaxError(f"Missing argument '{pname}' calling {func.__name__}")
+                bound_args[pname] = ast.Constant(p.default)
+        fscope = _Scope(_func_namespace(func), self.externals)
+        fscope.imported = dict(scope.imported)
+        for pname, arg in bound_args.items():
+            alias = None
+            if isinstance(arg, ast.Name) and (arg.id in scope.aliases or arg.id in scope.locals or (
+                scope is self._root_scope and (arg.id in self.fields or arg.id in self.scalars)
+            )):
+                e = self._resolve_name(arg.id, scope)
+                if isinstance(e, ir.FieldAccess):
+                    alias = ("field", e.name, e.offset)
+                else:
+                    alias = e
+            elif isinstance(arg, ast.Subscript) and isinstance(arg.value, ast.Name):
+                e = self._parse_expr(arg, scope, pre)
+                alias = ("field", e.name, e.offset) if isinstance(e, ir.FieldAccess) else e
+            else:
+                e = self._parse_expr(arg, scope, pre)
+                if isinstance(e, ir.Literal):
+                    alias = e
+                else:
+                    tname = self._new_temp_name(f"{func.__name__}_{pname}")
+                    self.temporaries[tname] = ir.FieldDecl(tname, DataType.AUTO, is_temporary=True)
+                    pre.append(ir.Assign(ir.FieldAccess(tname, (0, 0, 0)), e))
+                    alias = ("field", tname, (0, 0, 0))
+            fscope.aliases[pname] = alias
+        results = None
+        body = list(fdef.body)
+        if body and isinstance(body[0], ast.Expr) and isinstance(body[0].value, ast.Constant):
+            body = body[1:]
+        for st in body:
+            if isinstance(st, ast.Return):
+                if results is not None:
+                    raise GTScriptSyntaxError("Multiple return statements in gtscript function")
+                vals = st.value.elts if isinstance(st.value, ast.Tuple) else [st.value]
+                results = []
+                for v in vals:
+                    if isinstance(v, ast.Call) and is_gtscript_function(self._maybe_func(v, fscope)):
+                        results.extend(self._inline_call(v, fscope, pre, n_results=1))
+                    else:
+                        results.append(self._parse_expr(v, fscope, pre))
+            else:
+                pre.extend(self._parse_stmt_in_function(st, fscope))
+        if results is None:
+            raise GTScriptSyntaxError(f"gtscript function {func.__name__} has no return statement")
+        if len(results) != n_results:
+            raise GTScriptSyntaxError(
+                f"gtscript function {func.__name__} returns {len(results)} values, {n_results} expected"
+            )
+        return results
+
+    def _maybe_func(self, call: ast.Call, scope):
+        try:
+            if isinstance(call.func, ast.Name):
+                found, f = scope.lookup_external(call.func.id)
+                return f if found else None
+            return self._const_eval(call.func, scope)
+        except Exception:
+            return None
+
+    def _parse_stmt_in_function(self, st, fscope):
+        return self._parse_stmt(st, fscope)
+
+    # ------------------------------------------------------------------ public
+    def parse(self) -> ir.Stencil:
+        func = self.definition
+        self._parse_signature()
+        fdef = _func_ast(func)
+        scope = _Scope(_func_namespace(func), self.externals)
+        self._root_scope = scope
+        loops: List[ir.VerticalLoop] = []
+        body = list(fdef.body)
+        if body and isinstance(body[0], ast.Expr) and isinstance(getattr(body[0], "value", None), ast.Constant):
+            body = body[1:]
+        for stmt in body:
+            if isinstance(stmt, (ast.Import, ast.ImportFrom)):
+                self._parse_import(stmt, scope)
+            elif isinstance(stmt, ast.With):
+                loops.extend(self._parse_computation(stmt, scope))
+            elif isinstance(stmt, ast.Pass) or (
+                isinstance(stmt, ast.Expr) and isinstance(getattr(stmt, "value", None), ast.Constant)
+            ):
+                continue
+            else:
+                raise GTScriptSyntaxError(
+                    "Invalid stencil definition: only 'with computation(...)' blocks are allowed at the top "
+                    f"level (line {getattr(stmt, 'lineno', '?')})"
+                )
+        params: List[Any] = [self.fields[n] if n in self.fields else self.scalars[n] for n in self.api_order]
+        return ir.Stencil(
+            name=func.__name__,
+            api_signature=list(self.api_order),
+            params=params,
+            temporaries=list(self.temporaries.values()),
+            vertical_loops=loops,
+            externals=dict(self.used_externals),
+            docstring=inspect.getdoc(func) or "",
+        )
+
+
+def _load_copy(target):
+    """Turn an assignment target into an equivalent load expression."""
+    if isinstance(target, ast.Name):
+        return ast.Name(id=target.id, ctx=ast.Load())
+    if isinstance(target, ast.Subscript):
+        return ast.Subscript(value=_load_copy(target.value), slice=target.slice, ctx=ast.Load())
+    raise GTScriptSyntaxError("Invalid augmented assignment target")
+
+
+def parse_stencil(definition, externals, options) -> ir.Stencil:
+    parser = StencilParser(definition, externals, options)
+    stencil = parser.parse()
+    stencil.temp_declared_dtype = dict(parser.temp_declared_dtype)
+    return stencil

@@ -1,0 +1,132 @@
+"""Build orchestration: definition -> IR -> analysis -> backend class -> singleton instance.
+
+Plays the role of ``src/gt4py/cartesian/loader.py:30-69`` + ``stencil_builder.py:71-81`` +
+``backend/module_generator.py:56-106`` (``make_args_data_from_gtir``: ``FieldInfo``/
+``ParameterInfo``/``DomainInfo``). The stencil id hashes the typed IR (which already contains
+inlined functions and external values), the backend name, its versioned options and the
+literal precisions (cf. ``caching.py:300-327``).
+"""
+
+from __future__ import annotations
+
+import functools
+import inspect
+import time
+from typing import Any, Dict
+
+import numpy as np
+
+from gt4py_amd import frontend, passes
+from gt4py_amd.backend.base import from_name, stable_hash
+from gt4py_amd.definitions import AccessKind, Boundary, BuildOptions, DomainInfo, FieldInfo, ParameterInfo
+
+
+class StencilBuilder:
+    def __init__(self, definition, backend_cls, options: BuildOptions, externals: Dict[str, Any], dtypes):
+        self.definition = definition
+        self.backend_cls = backend_cls
+        self.options = options
+        self.externals = dict(externals or {})
+        self.dtypes = dict(dtypes or {})
+        if not self.options.name:
+            self.options.name = definition.__name__
+
+    @functools.cached_property
+    def ir(self):
+        t0 = time.perf_counter()
+        stencil = frontend.parse_stencil(self.definition, self.externals, self.options)
+        if self.options.build_info is not None:
+            self.options.build_info["parse_time"] = time.perf_counter() - t0
+        return stencil
+
+    @functools.cached_property
+    def analysis(self) -> passes.StencilAnalysis:
+        return passes.run_pipeline(self.ir)
+
+    @functools.cached_property
+    def stencil_id(self) -> str:
+        versioned = self.backend_cls.filter_options_for_id(self.options.backend_opts)
+        return stable_hash(
+            self.backend_cls.name,
+            self.analysis.stencil,
+            sorted(versioned.items()),
+            self.options.literal_int_precision,
+            self.options.literal_float_precision,
+            self.options.qualified_name,
+        )[:20]
+
+    @property
+    def class_name(self) -> str:
+        return f"{self.options.name}__{self.backend_cls.name.replace(':', '_')}_{self.stencil_id[:10]}"
+
+    @functools.cached_property
+    def source(self) -> str:
+        try:
+            return inspect.getsource(self.definition)
+        except OSError:
+            return ""
+
+    @functools.cached_property
+    def domain_info(self) -> DomainInfo:
+        return DomainInfo(
+            parallel_axes=("I", "J"), sequential_axis="K", min_sequential_axis_size=self.analysis.min_k_size, ndim=3
+        )
+
+    @functools.cached_property
+    def field_info(self) -> Dict[str, FieldInfo]:
+        a = self.analysis
+        out = {}
+        for f in a.stencil.field_params():
+            access = a.access.get(f.name, AccessKind.NONE)
+            if access != AccessKind.NONE:
+                bi, bj, bk = a.boundary(f.name)
+                boundary = Boundary((bi, bj, bk))
+            else:
+                boundary = Boundary(((0, 0), (0, 0), (0, 0)))
+            out[f.name] = FieldInfo(
+                access=access,
+                boundary=boundary,
+                axes=tuple(f.axes),
+                data_dims=tuple(f.data_dims),
+                dtype=f.dtype.np_dtype,
+            )
+        return out
+
+    @functools.cached_property
+    def parameter_info(self) -> Dict[str, ParameterInfo]:
+        a = self.analysis
+        return {
+            s.name: ParameterInfo(
+                access=AccessKind.READ if a.access.get(s.name, AccessKind.NONE) != AccessKind.NONE else AccessKind.NONE,
+                dtype=s.dtype.np_dtype,
+            )
+            for s in a.stencil.scalar_params()
+        }
+
+    @property
+    def constants(self) -> Dict[str, Any]:
+        return {k: v for k, v in self.analysis.stencil.externals.items() if isinstance(v, (bool, int, float, np.generic))}
+
+    @property
+    def options_dict(self) -> Dict[str, Any]:
+        return {
+            "name": self.options.name,
+            "module": self.options.module,
+            "format_source": self.options.format_source,
+            "backend_opts": dict(self.options.backend_opts),
+        }
+
+
+def load_stencil(definition, *, backend, build_options: BuildOptions, externals, dtypes):
+    backend_cls = from_name(backend)
+    builder = StencilBuilder(definition, backend_cls, build_options, externals, dtypes)
+    be = backend_cls(builder)
+    t0 = time.perf_counter()
+    cls = be.load()
+    if cls is None:
+        if build_options.raise_if_not_cached:
+            raise ValueError(f"The stencil {builder.options.name} is not up to date in the cache")
+        cls = be.generate()
+    elif build_options.build_info is not None:
+        build_options.build_info["load_time"] = time.perf_counter() - t0
+    return cls()

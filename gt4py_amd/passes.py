@@ -1,0 +1,478 @@
+"""Analysis and typing passes over ``gt4py_amd.ir``.
+
+Each pass restates the reference semantics it follows:
+
+- ``resolve_dtypes``: ``gtc/passes/gtir_dtype_resolver.py:17-84`` (temporaries take the dtype
+  of the right-hand side of their FIRST assignment) with the non-strict propagation of
+  ``gtc/common.py:285-305, 511-631`` (arithmetic -> max dtype, comparison -> bool, ...).
+- ``upcast``: ``gtc/passes/gtir_upcaster.py:42-147`` -- explicit ``Cast`` nodes chosen with the
+  NumPy-ufunc loop rule on the gt4py ``DataType`` ordering.
+- ``compute_access_kinds``: ``gtc/passes/oir_access_kinds.py:20-70`` (first access decides,
+  READ then WRITE -> READ_WRITE).
+- ``compute_extents``: ``gtc/passes/oir_optimizations/utils.py:250-330`` (reverse sweep over
+  horizontal executions; an execution's extent is the union of its written fields' extents).
+- ``compute_k_boundary`` / ``compute_min_k_size``: ``gtc/passes/gtir_k_boundary.py:24-109``.
+- ``validate_memory_accesses``: ``gtc/gtir_to_oir.py:19-47``.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import functools
+import math
+from typing import Dict, List, Optional, Set, Tuple
+
+import numpy as np
+
+from gt4py_amd import ir
+from gt4py_amd.definitions import AccessKind
+from gt4py_amd.ir import DataType
+
+# --------------------------------------------------------------------------------------
+# dtype propagation
+# --------------------------------------------------------------------------------------
+
+
+def _node_dtype(e: ir.Expr) -> DataType:
+    """(Re)compute the dtype of an expression node from its (typed) children."""
+    if isinstance(e, (ir.Literal, ir.FieldAccess, ir.ScalarAccess, ir.Cast, ir.AxisIndex)):
+        return e.dtype
+    if isinstance(e, ir.BinaryOp):
+        lt, rt = e.left.dtype, e.right.dtype
+        if e.op in ir.COMPARE_OPS:
+            return DataType.BOOL
+        if e.op in ir.LOGICAL_OPS:
+            if lt != DataType.BOOL or rt != DataType.BOOL:
+                raise TypeError("Arithmetic expression is not allowed in boolean operation.")
+            return DataType.BOOL
+        common = max(lt, rt)
+        if common == DataType.BOOL:
+            raise TypeError("Boolean expression is not allowed with arithmetic operation.")
+        return common
+    if isinstance(e, ir.UnaryOp):
+        if e.op == "not":
+            return DataType.BOOL
+        return e.expr.dtype
+    if isinstance(e, ir.TernaryOp):
+        return max(e.true_expr.dtype, e.false_expr.dtype)
+    if isinstance(e, ir.NativeCall):
+        f = e.func
+        if f in ("isfinite", "isinf", "isnan"):
+            return DataType.BOOL
+        if f in ("int32", "int64", "float32", "float64"):
+            return DataType[f.upper()]
+        return max(a.dtype for a in e.args)
+    raise TypeError(type(e))
+
+
+def resolve_dtypes(stencil: ir.Stencil) -> ir.Stencil:
+    """Propagate declaration dtypes to accesses and resolve temporaries (AUTO) in order."""
+    decls: Dict[str, object] = {p.name: p for p in stencil.params}
+    temp_dtype: Dict[str, DataType] = {}
+    declared = getattr(stencil, "temp_declared_dtype", {}) or {}
+    for t in stencil.temporaries:
+        decls[t.name] = t
+        if t.name in declared:
+            temp_dtype[t.name] = declared[t.name]
+
+    def type_expr(e: ir.Expr) -> ir.Expr:
+        if isinstance(e, ir.FieldAccess):
+            d = decls[e.name]
+            if getattr(d, "is_temporary", False):
+                if e.name not in temp_dtype:
+                    raise TypeError(f"Temporary '{e.name}' is read before being assigned")
+                return dataclasses.replace(e, dtype=temp_dtype[e.name])
+            return dataclasses.replace(e, dtype=d.dtype)
+        if isinstance(e, ir.ScalarAccess):
+            return dataclasses.replace(e, dtype=decls[e.name].dtype)
+        return _retype(e)
+
+    def visit_stmts(stmts):
+        out = []
+        for s in stmts:
+            if isinstance(s, ir.Assign):
+                value = ir.map_expr(s.value, type_expr)
+                name = s.target.name
+                d = decls[name]
+                if getattr(d, "is_temporary", False) and name not in temp_dtype:
+                    temp_dtype[name] = value.dtype
+                tgt = dataclasses.replace(
+                    s.target, dtype=temp_dtype[name] if getattr(d, "is_temporary", False) else d.dtype
+                )
+                out.append(ir.Assign(tgt, value))
+            elif isinstance(s, ir.If):
+                cond = ir.map_expr(s.cond, type_expr)
+                out.append(ir.If(cond, visit_stmts(s.body), visit_stmts(s.orelse)))
+            elif isinstance(s, ir.While):
+                cond = ir.map_expr(s.cond, type_expr)
+                out.append(ir.While(cond, visit_stmts(s.body)))
+            elif isinstance(s, ir.HorizontalRegion):
+                out.append(ir.HorizontalRegion(s.masks, visit_stmts(s.body)))
+            else:
+                raise TypeError(type(s))
+        return out
+
+    loops = []
+    for vl in stencil.vertical_loops:
+        secs = [ir.Section(sec.interval, visit_stmts(sec.body)) for sec in vl.sections]
+        loops.append(ir.VerticalLoop(vl.loop_order, secs))
+    temps = [dataclasses.replace(t, dtype=temp_dtype.get(t.name, DataType.FLOAT64)) for t in stencil.temporaries]
+    new = dataclasses.replace(stencil, vertical_loops=loops, temporaries=temps)
+    return new
+
+
+def _retype(e: ir.Expr) -> ir.Expr:
+    if isinstance(e, (ir.Literal, ir.FieldAccess, ir.ScalarAccess, ir.AxisIndex, ir.Cast)):
+        return e
+    return dataclasses.replace(e, dtype=_node_dtype(e))
+
+
+# --------------------------------------------------------------------------------------
+# upcasting (NumPy ufunc loop rule on the gt4py DataType ordering)
+# --------------------------------------------------------------------------------------
+
+_CUSTOM_UFUNC_TYPES = {
+    # gtc/ufuncs.py: scipy.special / custom functions registered with these loops
+    "gamma": ["f->f", "d->d"],
+    "erf": ["f->f", "d->d"],
+    "erfc": ["f->f", "d->d"],
+    "round": ["f->f", "d->d"],
+    "round_away_from_zero": ["f->f", "d->d"],
+}
+
+_OP_TO_UFUNC = {
+    "+": "add",
+    "-": "subtract",
+    "*": "multiply",
+    "/": "true_divide",
+    ">": "greater",
+    "<": "less",
+    ">=": "greater_equal",
+    "<=": "less_equal",
+    "==": "equal",
+    "!=": "not_equal",
+    "and": "logical_and",
+    "or": "logical_or",
+}
+_UNARY_TO_UFUNC = {"+": "positive", "-": "negative", "not": "logical_not"}
+_NATIVE_TO_UFUNC = {
+    "abs": "absolute",
+    "min": "minimum",
+    "max": "maximum",
+    "mod": "remainder",
+    "sin": "sin",
+    "cos": "cos",
+    "tan": "tan",
+    "arcsin": "arcsin",
+    "arccos": "arccos",
+    "arctan": "arctan",
+    "sinh": "sinh",
+    "cosh": "cosh",
+    "tanh": "tanh",
+    "arcsinh": "arcsinh",
+    "arccosh": "arccosh",
+    "arctanh": "arctanh",
+    "sqrt": "sqrt",
+    "exp": "exp",
+    "log": "log",
+    "log10": "log10",
+    "cbrt": "cbrt",
+    "isfinite": "isfinite",
+    "isinf": "isinf",
+    "isnan": "isnan",
+    "floor": "floor",
+    "ceil": "ceil",
+    "trunc": "trunc",
+}
+
+
+def _typechar_to_dt(ch: str) -> DataType:
+    try:
+        return DataType.from_np(np.dtype(ch))
+    except TypeError:
+        return DataType.INVALID
+
+
+@functools.lru_cache(maxsize=None)
+def _ufunc_types(name: str) -> Tuple[Tuple[Tuple[DataType, ...], DataType], ...]:
+    if name in _CUSTOM_UFUNC_TYPES:
+        types = _CUSTOM_UFUNC_TYPES[name]
+    else:
+        types = getattr(np, name).types
+    out = []
+    for t in types:
+        ins, outs = t.split("->")
+        out.append((tuple(_typechar_to_dt(c) for c in ins), _typechar_to_dt(outs[0])))
+    return tuple(out)
+
+
+@functools.lru_cache(maxsize=None)
+def ufunc_upcast(name: str, dtypes: Tuple[DataType, ...]) -> Tuple[DataType, ...]:
+    """``_numpy_ufunc_upcasting_rule`` (gtir_upcaster.py:42-70)."""
+    matched = {}
+    for ins, _ in _ufunc_types(name):
+        if len(ins) != len(dtypes):
+            continue
+        if any(c == DataType.INVALID for c in ins):
+            continue
+        if all(a <= c for a, c in zip(dtypes, ins)):
+            matched[sum(int(c) for c in ins)] = ins
+    if not matched:
+        raise TypeError(f"No '{name}' implementation for argument types {[d.name for d in dtypes]}")
+    return matched[min(matched)]
+
+
+def _cast(target: DataType, e: ir.Expr) -> ir.Expr:
+    return e if e.dtype == target else ir.Cast(target, e)
+
+
+def _upcast_expr(e: ir.Expr) -> ir.Expr:
+    if isinstance(e, ir.BinaryOp):
+        l, r = _upcast_expr(e.left), _upcast_expr(e.right)
+        tl, tr = ufunc_upcast(_OP_TO_UFUNC[e.op], (l.dtype, r.dtype))
+        return _retype(ir.BinaryOp(e.op, _cast(tl, l), _cast(tr, r)))
+    if isinstance(e, ir.UnaryOp):
+        x = _upcast_expr(e.expr)
+        (t,) = ufunc_upcast(_UNARY_TO_UFUNC[e.op], (x.dtype,))
+        return _retype(ir.UnaryOp(e.op, _cast(t, x)))
+    if isinstance(e, ir.TernaryOp):
+        c = _upcast_expr(e.cond)
+        t, f = _upcast_expr(e.true_expr), _upcast_expr(e.false_expr)
+        common = max(t.dtype, f.dtype)
+        return _retype(ir.TernaryOp(c, _cast(common, t), _cast(common, f)))
+    if isinstance(e, ir.NativeCall):
+        args = [_upcast_expr(a) for a in e.args]
+        if e.func in ("int32", "int64", "float32", "float64", "pow"):
+            return _retype(ir.NativeCall(e.func, args))
+        targets = ufunc_upcast(_NATIVE_TO_UFUNC.get(e.func, e.func), tuple(a.dtype for a in args))
+        return _retype(ir.NativeCall(e.func, [_cast(t, a) for t, a in zip(targets, args)]))
+    if isinstance(e, ir.Cast):
+        return ir.Cast(e.dtype, _upcast_expr(e.expr))
+    return e
+
+
+def upcast(stencil: ir.Stencil) -> ir.Stencil:
+    def visit_stmts(stmts):
+        out = []
+        for s in stmts:
+            if isinstance(s, ir.Assign):
+                v = _upcast_expr(s.value)
+                out.append(ir.Assign(s.target, _cast(s.target.dtype, v)))
+            elif isinstance(s, ir.If):
+                out.append(ir.If(_upcast_expr(s.cond), visit_stmts(s.body), visit_stmts(s.orelse)))
+            elif isinstance(s, ir.While):
+                out.append(ir.While(_upcast_expr(s.cond), visit_stmts(s.body)))
+            elif isinstance(s, ir.HorizontalRegion):
+                out.append(ir.HorizontalRegion(s.masks, visit_stmts(s.body)))
+            else:
+                raise TypeError(type(s))
+        return out
+
+    loops = [
+        ir.VerticalLoop(vl.loop_order, [ir.Section(sec.interval, visit_stmts(sec.body)) for sec in vl.sections])
+        for vl in stencil.vertical_loops
+    ]
+    return dataclasses.replace(stencil, vertical_loops=loops)
+
+
+# --------------------------------------------------------------------------------------
+# access helpers
+# --------------------------------------------------------------------------------------
+
+
+def stmt_writes(stmts) -> List[str]:
+    """Names assigned in a statement list (recursively), in program order."""
+    out: List[str] = []
+    for n in ir.walk(list(stmts)):
+        if isinstance(n, ir.Assign) and n.target.name not in out:
+            out.append(n.target.name)
+    return out
+
+
+def iter_accesses(stmts):
+    """Yield (FieldAccess|ScalarAccess, is_write) in the reference visiting order.
+
+    AssignStmt: right side first (READ), then the target (WRITE); If: condition, then
+    bodies; While: condition, then body (``oir_access_kinds.py:36-52``).
+    """
+
+    def expr_accesses(e):
+        for n in ir.walk(e):
+            if isinstance(n, (ir.FieldAccess, ir.ScalarAccess)):
+                yield n, False
+
+    def visit(s):
+        if isinstance(s, ir.Assign):
+            yield from expr_accesses(s.value)
+            yield s.target, True
+        elif isinstance(s, ir.If):
+            yield from expr_accesses(s.cond)
+            for x in s.body:
+                yield from visit(x)
+            for x in s.orelse:
+                yield from visit(x)
+        elif isinstance(s, ir.While):
+            yield from expr_accesses(s.cond)
+            for x in s.body:
+                yield from visit(x)
+        elif isinstance(s, ir.HorizontalRegion):
+            for x in s.body:
+                yield from visit(x)
+
+    for s in stmts:
+        yield from visit(s)
+
+
+def compute_access_kinds(stencil: ir.Stencil) -> Dict[str, AccessKind]:
+    access: Dict[str, AccessKind] = {}
+    for vl in stencil.vertical_loops:
+        for sec in vl.sections:
+            for acc, is_write in iter_accesses(sec.body):
+                kind = AccessKind.WRITE if is_write else AccessKind.READ
+                if kind == AccessKind.WRITE and access.get(acc.name) == AccessKind.READ:
+                    access[acc.name] = AccessKind.READ_WRITE
+                elif acc.name not in access:
+                    access[acc.name] = kind
+    for p in stencil.params:
+        access.setdefault(p.name, AccessKind.NONE)
+    return access
+
+
+# --------------------------------------------------------------------------------------
+# horizontal extents
+# --------------------------------------------------------------------------------------
+
+Extent = Tuple[Tuple[int, int], Tuple[int, int]]  # ((i_lo, i_hi), (j_lo, j_hi)) halo sizes >= 0
+ZERO_EXTENT: Extent = ((0, 0), (0, 0))
+
+
+def extent_union(a: Extent, b: Extent) -> Extent:
+    return ((max(a[0][0], b[0][0]), max(a[0][1], b[0][1])), (max(a[1][0], b[1][0]), max(a[1][1], b[1][1])))
+
+
+def extent_shift(e: Extent, offset) -> Extent:
+    di, dj = offset[0], offset[1]
+    return ((max(0, e[0][0] - di), max(0, e[0][1] + di)), (max(0, e[1][0] - dj), max(0, e[1][1] + dj)))
+
+
+@dataclasses.dataclass
+class ExtentInfo:
+    fields: Dict[str, Extent]
+    blocks: Dict[Tuple[int, int, int], Extent]  # (loop, section, statement) -> extent
+
+
+def compute_extents(stencil: ir.Stencil) -> ExtentInfo:
+    fields: Dict[str, Extent] = {}
+    blocks: Dict[Tuple[int, int, int], Extent] = {}
+    for li in reversed(range(len(stencil.vertical_loops))):
+        vl = stencil.vertical_loops[li]
+        for si in reversed(range(len(vl.sections))):
+            sec = vl.sections[si]
+            for ti in reversed(range(len(sec.body))):
+                stmt = sec.body[ti]
+                accesses = list(iter_accesses([stmt]))
+                he = ZERO_EXTENT
+                for acc, is_write in accesses:
+                    if is_write:
+                        he = extent_union(he, fields.setdefault(acc.name, ZERO_EXTENT))
+                blocks[(li, si, ti)] = he
+                for acc, is_write in accesses:
+                    if isinstance(acc, ir.FieldAccess):
+                        ext = extent_shift(he, acc.offset)
+                        fields[acc.name] = extent_union(fields.get(acc.name, ZERO_EXTENT), ext)
+    for p in stencil.params:
+        fields.setdefault(p.name, ZERO_EXTENT)
+    return ExtentInfo(fields, blocks)
+
+
+# --------------------------------------------------------------------------------------
+# K boundary and minimal K size
+# --------------------------------------------------------------------------------------
+
+
+def compute_k_boundary(stencil: ir.Stencil) -> Dict[str, Tuple[int, int]]:
+    temps = {t.name for t in stencil.temporaries}
+    bounds: Dict[str, List[float]] = {}
+    for vl in stencil.vertical_loops:
+        for sec in vl.sections:
+            itv = sec.interval
+            for acc, _ in iter_accesses(sec.body):
+                if not isinstance(acc, ir.FieldAccess):
+                    continue
+                b = bounds.setdefault(acc.name, [-math.inf, -math.inf])
+                k = acc.offset[2]
+                if itv.start.level == ir.LevelMarker.START:
+                    b[0] = max(-itv.start.offset - k, b[0])
+                if itv.end.level == ir.LevelMarker.END:
+                    b[1] = max(itv.end.offset + k, b[1])
+                if acc.name in temps and (b[0] > 0 or b[1] > 0):
+                    raise TypeError(f"Invalid access with offset in k to temporary field {acc.name}.")
+    out = {}
+    for name, b in bounds.items():
+        out[name] = (int(b[0]) if b[0] != -math.inf else 0, int(b[1]) if b[1] != -math.inf else 0)
+    for p in stencil.params:
+        out.setdefault(p.name, (0, 0))
+    return out
+
+
+def compute_min_k_size(stencil: ir.Stencil) -> int:
+    min_size_start = 0
+    min_size_end = 0
+    biggest_offset = 0
+    for vl in stencil.vertical_loops:
+        for sec in vl.sections:
+            s, e = sec.interval.start, sec.interval.end
+            if s.level == ir.LevelMarker.START and e.level == ir.LevelMarker.END:
+                if not (s.offset == 0 and e.offset == 0):
+                    biggest_offset = max(biggest_offset, s.offset - e.offset + 1)
+            elif s.level == ir.LevelMarker.START and e.level == ir.LevelMarker.START:
+                min_size_start = max(min_size_start, e.offset)
+                biggest_offset = max(biggest_offset, e.offset)
+            else:
+                min_size_end = max(min_size_end, -s.offset)
+                biggest_offset = max(biggest_offset, -s.offset)
+    return max(min_size_start + min_size_end, biggest_offset)
+
+
+def validate_memory_accesses(stencil: ir.Stencil, extents: ExtentInfo) -> None:
+    field_names = {p.name for p in stencil.field_params()}
+    written: Set[str] = set()
+    for vl in stencil.vertical_loops:
+        for sec in vl.sections:
+            written.update(stmt_writes(sec.body))
+    bad = sorted(n for n in written & field_names if extents.fields[n] != ZERO_EXTENT)
+    if bad:
+        raise ValueError(f"Found non-zero read extent on written fields: {', '.join(bad)}")
+
+
+# --------------------------------------------------------------------------------------
+# Pipeline
+# --------------------------------------------------------------------------------------
+
+
+@dataclasses.dataclass
+class StencilAnalysis:
+    stencil: ir.Stencil
+    access: Dict[str, AccessKind]
+    extents: ExtentInfo
+    k_boundary: Dict[str, Tuple[int, int]]
+    min_k_size: int
+
+    def boundary(self, name: str):
+        e = self.extents.fields.get(name, ZERO_EXTENT)
+        return (e[0], e[1], self.k_boundary.get(name, (0, 0)))
+
+
+def prune_unused_fields(stencil: ir.Stencil) -> ir.Stencil:
+    return stencil
+
+
+def run_pipeline(stencil: ir.Stencil) -> StencilAnalysis:
+    stencil = resolve_dtypes(stencil)
+    stencil = upcast(stencil)
+    extents = compute_extents(stencil)
+    validate_memory_accesses(stencil, extents)
+    access = compute_access_kinds(stencil)
+    kb = compute_k_boundary(stencil)
+    min_k = compute_min_k_size(stencil)
+    return StencilAnalysis(stencil, access, extents, kb, min_k)

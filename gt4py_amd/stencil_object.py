@@ -1,0 +1,488 @@
+"""Runtime call path: ``StencilObject`` / ``FrozenStencil``.
+
+Same contract as ``src/gt4py/cartesian/stencil_object.py``:
+- singleton, frozen subclasses (``:194-204``),
+- ``_call_run`` (``:534-605``): extract arrays, domain/origin cache keyed like ``:38-49``,
+  ``_normalize_origins`` (``:499-532``), ``_get_max_domain`` (``:298-343``),
+  ``_validate_args`` (``:345-497``) with the same error types and messages,
+- ``freeze`` -> ``FrozenStencil`` (``:94-128``) which skips validation,
+- ``exec_info`` timestamps and ``__aggregate_data`` counters
+  (``backend/templates/stencil_module.py.in:91-169``).
+
+Arrays are borrowed. Device arrays are torch tensors (ROCm) or any object exposing
+``__cuda_array_interface__``; host arrays are numpy arrays.
+"""
+
+from __future__ import annotations
+
+import abc
+import collections.abc
+import sys
+import time
+import warnings
+from dataclasses import dataclass
+from pickle import dumps
+from typing import Any, Callable, ClassVar, Dict, Optional, Tuple
+
+import numpy as np
+
+from gt4py_amd import definitions as gd
+from gt4py_amd.definitions import AccessKind, DomainInfo, FieldInfo, ParameterInfo
+from gt4py_amd.storage import array_info as storage_array_info
+
+
+@dataclass
+class ArgsInfo:
+    device: str
+    array: Any
+    original_object: Any = None
+    origin: Optional[Tuple[int, ...]] = None
+    dimensions: Optional[Tuple[str, ...]] = None
+
+    @property
+    def shape(self):
+        return tuple(self.array.shape)
+
+
+def _compute_domain_origin_cache_key(field_args_info, parameter_args, domain, origin) -> int:
+    field_data = tuple(
+        (name, tuple(arg.array.shape), arg.origin or (0, 0, 0)) for name, arg in field_args_info.items() if arg is not None
+    )
+    return hash((field_data, *parameter_args.keys(), dumps(domain), dumps(origin)))
+
+
+def _extract_array_infos(field_args, device) -> Dict[str, Optional[ArgsInfo]]:
+    infos: Dict[str, Optional[ArgsInfo]] = {}
+    for name, arg in field_args.items():
+        if arg is None:
+            infos[name] = None
+            continue
+        array, dims, origin = storage_array_info(arg)
+        if dims is not None:
+            sorted_dims = [d for d in "IJK" if d in dims]
+            data_dims = sorted(int(d) for d in dims if str(d).isdigit())
+            sorted_dims += [str(d) for d in data_dims]
+            perm = [dims.index(sd) for sd in sorted_dims]
+            if perm != list(range(len(perm))):
+                array = array.permute(*perm) if hasattr(array, "permute") else array.transpose(perm)
+            dims = tuple(sorted_dims)
+        infos[name] = ArgsInfo(device=device, array=array, original_object=arg, dimensions=dims, origin=origin)
+    return infos
+
+
+def _nt_lt(a, b) -> bool:
+    """NumericTuple '<': no element greater and at least one smaller (gtc/definitions.py:141-147)."""
+    return any(x < y for x, y in zip(a, b)) and not any(x > y for x, y in zip(a, b))
+
+
+def _nt_gt(a, b) -> bool:
+    return any(x > y for x, y in zip(a, b)) and not any(x < y for x, y in zip(a, b))
+
+
+def _nt_le(a, b) -> bool:
+    return all(x <= y for x, y in zip(a, b))
+
+
+@dataclass(frozen=True)
+class FrozenStencil:
+    """Stencil with pre-computed domain and origin for each field argument."""
+
+    stencil_object: "StencilObject"
+    origin: Dict[str, Tuple[int, ...]]
+    domain: Tuple[int, ...]
+
+    def __post_init__(self):
+        for name, field_info in self.stencil_object.field_info.items():
+            if name not in self.origin or len(self.origin[name]) != field_info.ndim:
+                raise ValueError(
+                    f"'{name}' origin {self.origin.get(name)} is not a {field_info.ndim}-dimensional integer tuple"
+                )
+
+    def __call__(self, **kwargs) -> None:
+        assert "origin" not in kwargs and "domain" not in kwargs
+        exec_info = kwargs.get("exec_info")
+        if exec_info is not None:
+            exec_info["call_run_start_time"] = time.perf_counter()
+        field_args = {name: kwargs[name] for name in self.stencil_object.field_info.keys()}
+        parameter_args = {name: kwargs[name] for name in self.stencil_object.parameter_info.keys()}
+        self.stencil_object.run(
+            _domain_=self.domain, _origin_=self.origin, exec_info=exec_info, **field_args, **parameter_args
+        )
+        if exec_info is not None:
+            exec_info["call_run_end_time"] = time.perf_counter()
+
+
+class StencilObject(abc.ABC):
+    """Generic singleton implementation of a stencil callable (see module docstring)."""
+
+    _gt_id_: str
+    definition_func: Callable[..., Any]
+    _domain_origin_cache: ClassVar[Dict[int, Tuple[Tuple[int, ...], Dict[str, Tuple[int, ...]]]]]
+
+    # filled in by the backend's class factory
+    _gt_backend_: ClassVar[str]
+    _gt_source_: ClassVar[str]
+    _gt_domain_info_: ClassVar[DomainInfo]
+    _gt_field_info_: ClassVar[Dict[str, FieldInfo]]
+    _gt_parameter_info_: ClassVar[Dict[str, ParameterInfo]]
+    _gt_constants_: ClassVar[Dict[str, Any]]
+    _gt_options_: ClassVar[Dict[str, Any]]
+
+    def __new__(cls, *args, **kwargs):
+        if cls.__dict__.get("_instance") is None:
+            inst = object.__new__(cls)
+            type.__setattr__(cls, "_instance", inst)
+            type.__setattr__(cls, "_domain_origin_cache", {})
+        return cls.__dict__["_instance"]
+
+    def __setattr__(self, key, value) -> None:
+        raise AttributeError("Attempting a modification of an attribute in a frozen class")
+
+    def __delattr__(self, item) -> None:
+        raise AttributeError("Attempting a deletion of an attribute in a frozen class")
+
+    def __eq__(self, other) -> bool:
+        return type(self) is type(other)
+
+    def __hash__(self) -> int:
+        return int.from_bytes(type(self)._gt_id_.encode()[:16], byteorder="little")
+
+    def __str__(self) -> str:
+        return (
+            f"<StencilObject: {self.options['module']}.{self.options['name']}> [backend=\"{self.backend}\"]\n"
+            f"    - I/O fields: {self.field_info}\n    - Parameters: {self.parameter_info}\n"
+            f"    - Constants: {self.constants}\n    - Version: {self._gt_id_}\n"
+        )
+
+    @property
+    def backend(self) -> str:
+        return type(self)._gt_backend_
+
+    @property
+    def source(self) -> str:
+        return type(self)._gt_source_
+
+    @property
+    def domain_info(self) -> DomainInfo:
+        return type(self)._gt_domain_info_
+
+    @property
+    def field_info(self) -> Dict[str, FieldInfo]:
+        return type(self)._gt_field_info_
+
+    @property
+    def parameter_info(self) -> Dict[str, ParameterInfo]:
+        return type(self)._gt_parameter_info_
+
+    @property
+    def constants(self) -> Dict[str, Any]:
+        return type(self)._gt_constants_
+
+    @property
+    def options(self) -> Dict[str, Any]:
+        return type(self)._gt_options_
+
+    @abc.abstractmethod
+    def run(self, _domain_, _origin_, exec_info, **kwargs) -> None:
+        pass
+
+    # ------------------------------------------------------------------ call path
+    def _call_impl(self, field_args, parameter_args, domain, origin, validate_args, exec_info):
+        if exec_info is not None:
+            exec_info["call_start_time"] = time.perf_counter()
+        self._call_run(
+            field_args=field_args,
+            parameter_args=parameter_args,
+            domain=domain,
+            origin=origin,
+            validate_args=validate_args,
+            exec_info=exec_info,
+        )
+        if exec_info is not None:
+            exec_info["call_end_time"] = time.perf_counter()
+            if exec_info.setdefault("__aggregate_data", False):
+                info = exec_info.setdefault(type(self).__name__, {})
+                info["call_start_time"] = exec_info["call_start_time"]
+                info["call_end_time"] = exec_info["call_end_time"]
+                info["call_time"] = info["call_end_time"] - info["call_start_time"]
+                info["total_call_time"] = info.get("total_call_time", 0.0) + info["call_time"]
+                info["ncalls"] = info.get("ncalls", 0) + 1
+                info["run_time"] = exec_info["run_end_time"] - exec_info["run_start_time"]
+                info["total_run_time"] = info.get("total_run_time", 0.0) + info["run_time"]
+                if "run_cpp_start_time" in exec_info:
+                    info["run_cpp_time"] = exec_info["run_cpp_end_time"] - exec_info["run_cpp_start_time"]
+                    info["total_run_cpp_time"] = info.get("total_run_cpp_time", 0.0) + info["run_cpp_time"]
+
+    @staticmethod
+    def _make_origin_dict(origin) -> Dict[str, Tuple[int, ...]]:
+        try:
+            if isinstance(origin, dict):
+                return {str(k): tuple(v) for k, v in origin.items()}
+            if origin is None:
+                return {}
+            if isinstance(origin, collections.abc.Iterable):
+                return {"_all_": tuple(int(x) for x in origin)}
+            if isinstance(origin, int):
+                return {"_all_": (0, 0, origin)}
+        except Exception:
+            pass
+        raise ValueError("Invalid 'origin' value ({})".format(origin))
+
+    @staticmethod
+    def _get_max_domain(array_infos, domain_infos, field_infos, origin, *, squeeze=True):
+        domain_ndim = domain_infos.ndim
+        max_size = sys.maxsize
+        max_domain = [max_size] * domain_ndim
+        for name, field_info in field_infos.items():
+            if field_info.access != AccessKind.NONE:
+                info = array_infos.get(name, None)
+                assert info is not None, f"Invalid value for '{name}' field."
+                mask = field_info.domain_mask
+                upper = gd.filter_mask(field_info.boundary.upper_indices, mask)
+                forigin = tuple(origin[name])
+                fdomain = tuple(info.shape[i] - (forigin[i] + upper[i]) for i in range(field_info.domain_ndim))
+                full = gd.interpolate_mask(fdomain, mask, max_size)
+                max_domain = [min(a, b) for a, b in zip(max_domain, full)]
+        if squeeze:
+            return tuple(i if i != max_size else 1 for i in max_domain)
+        return tuple(max_domain)
+
+    def _validate_args(self, arg_infos, param_args, domain, origin) -> None:
+        from gt4py_amd.backend import from_name
+
+        domain_ndim = self.domain_info.ndim
+        if len(domain) != domain_ndim:
+            raise ValueError(f"Invalid 'domain' value '{domain}'")
+        try:
+            domain = tuple(int(d) for d in domain)
+        except Exception as ex:
+            raise ValueError("Invalid 'domain' value ({})".format(domain)) from ex
+        if not _nt_gt(domain, (0,) * domain_ndim):
+            raise ValueError(f"Compute domain contains zero sizes '{domain}')")
+        max_domain = self._get_max_domain(arg_infos, self.domain_info, self.field_info, origin, squeeze=False)
+        if not _nt_le(domain, max_domain):
+            offending = []
+            for name, info in self.field_info.items():
+                used = self._get_max_domain(arg_infos, self.domain_info, {name: info}, origin, squeeze=False)
+                if _nt_lt(used, domain):
+                    offending.append((name, used))
+            raise ValueError(
+                f"Compute domain too large for stencil {self.options['name']}: \n"
+                f"  Stencil domain is {domain} but field indexation leads to read outside of bounds.\n"
+                f"  Check region/horizontal offsets or interval/vertical offsets, or stencil domain.\n"
+                f"  Offending fields (name, size with offset removed): {offending}"
+            )
+        if domain[2] < self.domain_info.min_sequential_axis_size:
+            raise ValueError(
+                f"Compute domain too small. Sequential axis is {domain[2]}, but must be at least "
+                f"{self.domain_info.min_sequential_axis_size}."
+            )
+        backend_cls = from_name(self.backend)
+        for name, field_info in self.field_info.items():
+            if field_info.access == AccessKind.NONE:
+                continue
+            if name not in arg_infos or arg_infos[name] is None:
+                raise ValueError(f"Missing value for '{name}' field.")
+            arg_info = arg_infos[name]
+            dims = tuple(list(field_info.axes) + [str(d) for d in range(len(field_info.data_dims))])
+            if not backend_cls.storage_info["is_optimal_layout"](arg_info.array, dims):
+                warnings.warn(
+                    f"The layout of the field '{name}' is not recommended for this backend."
+                    f"This may lead to performance degradation. Please consider using the"
+                    f"provided allocators in `gt4py_amd.storage`.",
+                    stacklevel=2,
+                )
+            adtype = _array_dtype(arg_info.array)
+            if adtype != field_info.dtype:
+                raise TypeError(f"The dtype of field '{name}' is '{adtype}' instead of '{field_info.dtype}'")
+            mask = field_info.domain_mask
+            fndim = field_info.domain_ndim
+            forigin = gd.filter_mask(origin[name], mask[:domain_ndim]) if len(origin[name]) == 3 else tuple(
+                origin[name][:fndim]
+            )
+            if len(arg_info.shape) != fndim + len(field_info.data_dims):
+                raise ValueError(
+                    f"Storage for '{name}' has {len(arg_info.shape)} dimensions but the API signature "
+                    f"expects {fndim + len(field_info.data_dims)} ('{field_info.axes}[{field_info.data_dims}]')"
+                )
+            if arg_info.dimensions is not None and (
+                *field_info.axes,
+                *(str(d) for d in range(len(field_info.data_dims))),
+            ) != tuple(arg_info.dimensions):
+                raise ValueError(
+                    f"Storage for '{name}' has dimensions '{arg_info.dimensions}' but the API signature "
+                    f"expects '[{', '.join(field_info.axes)}]'"
+                    + (f" and {len(field_info.data_dims)}" if field_info.data_dims else "")
+                )
+            if tuple(arg_info.shape[fndim:]) != tuple(field_info.data_dims):
+                raise ValueError(
+                    f"Field '{name}' expects data dimensions {field_info.data_dims} but got "
+                    f"{tuple(arg_info.shape[fndim:])}"
+                )
+            lower = gd.filter_mask(field_info.boundary.lower_indices, mask)
+            min_origin = gd.interpolate_mask(lower, mask, 0)
+            forigin_full = gd.interpolate_mask(forigin, mask, 0)
+            if _nt_lt(forigin_full, min_origin):
+                raise ValueError(
+                    f"Origin for field {name} too small. Must be at least {min_origin}, is {forigin_full}"
+                )
+            spatial = gd.filter_mask(domain, mask)
+            upper = gd.filter_mask(field_info.boundary.upper_indices, mask)
+            min_shape = tuple(lb + d + ub for lb, d, ub in zip(lower, spatial, upper))
+            if min_shape > tuple(arg_info.shape):
+                raise ValueError(
+                    f"Shape of field {name} is {tuple(arg_info.shape)} but must be at least {min_shape} "
+                    f"for given domain and origin."
+                )
+        for name, parameter_info in self.parameter_info.items():
+            if parameter_info.access != AccessKind.NONE:
+                if name not in param_args:
+                    raise ValueError(f"Missing value for '{name}' parameter.")
+                parameter = param_args[name]
+                if np.dtype(type(parameter)) != parameter_info.dtype:
+                    raise TypeError(
+                        f"The type of parameter '{name}' is '{type(parameter)}' instead of '{parameter_info.dtype}'"
+                    )
+
+    @staticmethod
+    def _normalize_origins(array_infos, field_infos, origin) -> Dict[str, Tuple[int, ...]]:
+        origin = StencilObject._make_origin_dict(origin)
+        all_origin = origin.get("_all_", None)
+        for name, field_info in field_infos.items():
+            assert name in array_infos, f"Missing value for '{name}' field."
+            field_origin = origin.get(name, None)
+            if field_origin is not None:
+                if len(field_origin) != field_info.ndim:
+                    assert len(field_origin) == field_info.domain_ndim, (
+                        f"Invalid origin specification ({field_origin}) for '{name}' field."
+                    )
+                    origin[name] = (*field_origin, *((0,) * len(field_info.data_dims)))
+            elif all_origin is not None:
+                origin[name] = (
+                    *gd.filter_mask(all_origin, field_info.domain_mask),
+                    *((0,) * len(field_info.data_dims)),
+                )
+            elif (info_origin := getattr(array_infos.get(name), "origin", None)) is not None:
+                origin[name] = tuple(info_origin)
+            else:
+                origin[name] = (0,) * field_info.ndim
+        return origin
+
+    def _call_run(self, field_args, parameter_args, domain, origin, *, validate_args=True, exec_info=None):
+        if exec_info is not None:
+            exec_info["call_run_start_time"] = time.perf_counter()
+        from gt4py_amd.backend import from_name
+
+        device = from_name(self.backend).storage_info["device"]
+        array_infos = _extract_array_infos(field_args, device)
+        cache_key = _compute_domain_origin_cache_key(array_infos, parameter_args, domain, origin)
+        cache = type(self)._domain_origin_cache
+        if cache_key not in cache:
+            origin = self._normalize_origins(array_infos, self.field_info, origin)
+            if domain is None:
+                domain = self._get_max_domain(array_infos, self.domain_info, self.field_info, origin)
+            if validate_args:
+                self._validate_args(array_infos, parameter_args, domain, origin)
+            cache[cache_key] = (domain, origin)
+        else:
+            domain, origin = cache[cache_key]
+        arrays = {name: (info.array if info is not None else None) for name, info in array_infos.items()}
+        self.run(_domain_=domain, _origin_=origin, exec_info=exec_info, **arrays, **parameter_args)
+        if exec_info is not None:
+            exec_info["call_run_end_time"] = time.perf_counter()
+
+    def freeze(self, *, origin: Dict[str, Tuple[int, ...]], domain: Tuple[int, ...]) -> FrozenStencil:
+        return FrozenStencil(self, origin, domain)
+
+    def clean_call_args_cache(self) -> None:
+        type(self)._domain_origin_cache.clear()
+
+    def __deepcopy__(self, memodict=None):
+        return self
+
+
+def _array_dtype(array) -> np.dtype:
+    dt = getattr(array, "dtype", None)
+    if isinstance(dt, np.dtype):
+        return dt
+    try:
+        import torch
+
+        if isinstance(dt, torch.dtype):
+            return np.dtype(str(dt).replace("torch.", "").replace("bool", "bool_"))
+    except ImportError:  # pragma: no cover
+        pass
+    return np.dtype(dt)
+
+
+def make_stencil_class(
+    *,
+    class_name: str,
+    backend_name: str,
+    stencil_id: str,
+    definition_func,
+    source: str,
+    domain_info: DomainInfo,
+    field_info: Dict[str, FieldInfo],
+    parameter_info: Dict[str, ParameterInfo],
+    constants: Dict[str, Any],
+    options: Dict[str, Any],
+    run_impl: Callable,
+    module: str,
+) -> type:
+    """Create the per-stencil ``StencilObject`` subclass.
+
+    ``__call__`` gets the definition's own signature (as the reference template does,
+    ``stencil_module.py.in:91-93``) plus ``domain=None, origin=None, validate_args=True,
+    exec_info=None``.
+    """
+    import inspect
+
+    sig = inspect.signature(definition_func)
+    field_names = [n for n in sig.parameters if n in field_info]
+    param_names = [n for n in sig.parameters if n in parameter_info]
+    parts = []
+    seen_kwonly = False
+    for p in sig.parameters.values():
+        if p.kind == p.KEYWORD_ONLY and not seen_kwonly:
+            parts.append("*")
+            seen_kwonly = True
+        parts.append(f"{p.name}=None" if p.default is None else p.name)
+    if not seen_kwonly:
+        parts.append("*")
+    parts += ["domain=None", "origin=None", "validate_args=True", "exec_info=None"]
+    fdict = ", ".join(f"{n}={n}" for n in field_names)
+    pdict = ", ".join(f"{n}={n}" for n in param_names)
+    src = (
+        f"def __call__(self, {', '.join(parts)}):\n"
+        f"    self._call_impl(dict({fdict}), dict({pdict}), domain, origin, validate_args, exec_info)\n"
+    )
+    ns: Dict[str, Any] = {}
+    exec(compile(src, f"<gt4py_amd:{class_name}.__call__>", "exec"), ns)  # noqa: S102 - generated code
+
+    def run(self, _domain_, _origin_, exec_info, **kwargs):
+        if exec_info is not None:
+            exec_info["domain"] = _domain_
+            exec_info["origin"] = _origin_
+            exec_info["run_start_time"] = time.perf_counter()
+        run_impl(_domain_, _origin_, exec_info, kwargs)
+        if exec_info is not None:
+            exec_info["run_end_time"] = time.perf_counter()
+
+    attrs = {
+        "__call__": ns["__call__"],
+        "run": run,
+        "_gt_backend_": backend_name,
+        "_gt_source_": source,
+        "_gt_domain_info_": domain_info,
+        "_gt_field_info_": field_info,
+        "_gt_parameter_info_": parameter_info,
+        "_gt_constants_": constants,
+        "_gt_options_": options,
+        "_gt_id_": stencil_id,
+        "definition_func": staticmethod(definition_func),
+        "__module__": module,
+        "__doc__": inspect.getdoc(definition_func) or "",
+        "_instance": None,
+    }
+    return type(class_name, (StencilObject,), attrs)

@@ -1,0 +1,1157 @@
+"""Stencil cases shared by the golden-fixture generator and the parity tests.
+
+Every case is a GTScript definition written against ``gt4py_amd.gtscript`` plus a
+deterministic input recipe (shapes, dtypes, value ranges, origin, domain, parameters).
+
+``tests/golden/make_golden.py`` runs each definition through the *reference* numpy
+backend (``gt4py.cartesian``, only in the build container) by aliasing
+``gt4py_amd.gtscript`` to the reference module, and stores inputs + outputs as ``.npz``.
+The parity tests build the very same definitions with ``gt4py_amd`` backends and compare.
+
+The stencils restate the GTScript programs of the reference's own tests:
+- ``tests/cartesian_tests/integration_tests/multi_feature_tests/stencil_definitions.py``
+- ``tests/cartesian_tests/integration_tests/multi_feature_tests/test_suites.py``
+- the demo notebook ``examples/cartesian/demo_horizontal_diffusion.ipynb`` (cells 7/9)
+"""
+
+
+
+import dataclasses
+import zlib
+from typing import Any, Callable, Dict, Optional, Tuple
+
+import numpy as np
+
+from gt4py_amd import gtscript
+from gt4py_amd.gtscript import (
+    BACKWARD,
+    FORWARD,
+    PARALLEL,
+    Field,
+    I,
+    J,
+    computation,
+    horizontal,
+    interval,
+    region,
+)
+from gt4py_amd.gtscript import __INLINED  # noqa: F401  (used inside stencil bodies)
+from gt4py_amd.gtscript import (  # noqa: F401  (math builtins used inside stencil bodies)
+    acos,
+    acosh,
+    asin,
+    asinh,
+    atan,
+    atanh,
+    cbrt,
+    ceil,
+    cos,
+    cosh,
+    erf,
+    erfc,
+    exp,
+    floor,
+    gamma,
+    isfinite,
+    isinf,
+    isnan,
+    log,
+    log10,
+    mod,
+    round,
+    round_away_from_zero,
+    sin,
+    sinh,
+    sqrt,
+    tan,
+    tanh,
+    trunc,
+)
+
+F64 = Field[np.float64]
+F32 = Field[np.float32]
+FBool = Field[np.bool_]
+F2D = Field[gtscript.IJ, np.float64]
+
+
+@dataclasses.dataclass
+class FieldSpec:
+    shape: Tuple[int, ...]
+    dtype: str = "f8"
+    init: Any = ("u", -10.0, 10.0)  # ("u", lo, hi) | ("int", lo, hi) | "bool" | "zeros" | "demo" | ("const", v)
+    nan_frac: float = 0.0
+
+
+@dataclasses.dataclass
+class Case:
+    name: str
+    definition: Callable
+    fields: Dict[str, Optional[FieldSpec]]
+    params: Dict[str, Any]
+    externals: Dict[str, Any]
+    origin: Any
+    domain: Optional[Tuple[int, int, int]]
+    rtol: float = 0.0  # 0 => bit-exact expected on every backend
+    atol: float = 0.0
+    features: Tuple[str, ...] = ()  # tags used by tests to select/skip cases
+
+    @property
+    def seed(self) -> int:
+        return zlib.crc32(self.name.encode()) & 0x7FFFFFFF
+
+    def make_inputs(self) -> Dict[str, Optional[np.ndarray]]:
+        rng = np.random.default_rng(self.seed)
+        out: Dict[str, Optional[np.ndarray]] = {}
+        for name, spec in self.fields.items():
+            if spec is None:
+                out[name] = None
+                continue
+            out[name] = _make_array(spec, rng)
+        return out
+
+
+def _make_array(spec: FieldSpec, rng: np.random.Generator) -> np.ndarray:
+    dt = np.dtype(spec.dtype)
+    init = spec.init
+    shape = tuple(spec.shape)
+    if init == "zeros":
+        arr = np.zeros(shape, dtype=dt)
+    elif init == "bool":
+        arr = rng.random(shape) > 0.5
+    elif init == "demo":
+        # demo_horizontal_diffusion.ipynb cell 9: in = 5 + 8*(2 + cos(pi*(x+1.5y)) + sin(2pi*(x+1.5y)))/4
+        ni, nj = shape[0], shape[1]
+        x = np.arange(ni)[:, None] / ni
+        y = np.arange(nj)[None, :] / nj
+        plane = 5.0 + 8.0 * (2.0 + np.cos(np.pi * (x + 1.5 * y)) + np.sin(2 * np.pi * (x + 1.5 * y))) / 4.0
+        arr = np.empty(shape, dtype=np.float64)
+        arr[...] = plane[:, :, None] if len(shape) == 3 else plane
+    elif isinstance(init, tuple) and init[0] == "u":
+        arr = rng.uniform(init[1], init[2], size=shape)
+    elif isinstance(init, tuple) and init[0] == "int":
+        arr = rng.integers(init[1], init[2], size=shape)
+    elif isinstance(init, tuple) and init[0] == "const":
+        arr = np.full(shape, init[1])
+    else:
+        raise ValueError(f"unknown init {init!r}")
+    arr = np.asarray(arr).astype(dt)
+    if spec.nan_frac:
+        flat = arr.reshape(-1)
+        n = max(1, int(spec.nan_frac * flat.size))
+        idx = rng.choice(flat.size, size=3 * n, replace=False)
+        flat[idx[:n]] = np.nan
+        flat[idx[n : 2 * n]] = np.inf
+        flat[idx[2 * n :]] = -np.inf
+    return arr
+
+
+CASES: Dict[str, Case] = {}
+
+
+def case(
+    name: Optional[str] = None,
+    *,
+    fields,
+    params=None,
+    externals=None,
+    origin=None,
+    domain=None,
+    rtol=0.0,
+    atol=0.0,
+    features=(),
+):
+    def deco(func):
+        n = name or func.__name__
+        assert n not in CASES, n
+        CASES[n] = Case(
+            n,
+            func,
+            dict(fields),
+            dict(params or {}),
+            dict(externals or {}),
+            origin,
+            domain,
+            rtol,
+            atol,
+            tuple(features),
+        )
+        return func
+
+    return deco
+
+
+def fs(*shape, dtype="f8", init=("u", -10.0, 10.0), nan_frac=0.0):
+    return FieldSpec(tuple(shape), dtype, init, nan_frac)
+
+
+# --------------------------------------------------------------------------------------
+# Hot-path stencils
+# --------------------------------------------------------------------------------------
+
+
+def copy_stencil(field_a: F64, field_b: F64):
+    with computation(PARALLEL), interval(...):
+        field_b = field_a[0, 0, 0]
+
+
+case("copy", fields={"field_a": fs(16, 12, 8), "field_b": fs(16, 12, 8)}, features=("hot",))(copy_stencil)
+case(
+    "copy_subdomain",
+    fields={"field_a": fs(16, 12, 8), "field_b": fs(16, 12, 8)},
+    origin=(1, 2, 1),
+    domain=(10, 8, 5),
+    features=("hot",),
+)(copy_stencil)
+
+
+def lap5(in_field: F64, out_field: F64):
+    with computation(PARALLEL), interval(...):
+        out_field = 4.0 * in_field[0, 0, 0] - (
+            in_field[1, 0, 0] + in_field[-1, 0, 0] + in_field[0, 1, 0] + in_field[0, -1, 0]
+        )
+
+
+case(
+    "lap5",
+    fields={"in_field": fs(26, 22, 8), "out_field": fs(24, 20, 8, init="zeros")},
+    origin={"in_field": (1, 1, 0), "out_field": (0, 0, 0)},
+    domain=(24, 20, 8),
+    features=("hot",),
+)(lap5)
+
+
+def _hdiff_body_factory(dtype):
+    FT = Field[dtype]
+
+    def horizontal_diffusion(in_field: FT, out_field: FT, coeff: FT):
+        with computation(PARALLEL), interval(...):
+            lap_field = 4.0 * in_field[0, 0, 0] - (
+                in_field[1, 0, 0] + in_field[-1, 0, 0] + in_field[0, 1, 0] + in_field[0, -1, 0]
+            )
+            res = lap_field[1, 0, 0] - lap_field[0, 0, 0]
+            flx_field = 0 if (res * (in_field[1, 0, 0] - in_field[0, 0, 0])) > 0 else res
+            res = lap_field[0, 1, 0] - lap_field[0, 0, 0]
+            fly_field = 0 if (res * (in_field[0, 1, 0] - in_field[0, 0, 0])) > 0 else res
+            out_field = in_field[0, 0, 0] - coeff[0, 0, 0] * (
+                flx_field[0, 0, 0] - flx_field[-1, 0, 0] + fly_field[0, 0, 0] - fly_field[0, -1, 0]
+            )
+
+    return horizontal_diffusion
+
+
+hdiff_f64 = _hdiff_body_factory(np.float64)
+hdiff_f32 = _hdiff_body_factory(np.float32)
+
+_HD_ORIGIN = {"in_field": (2, 2, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+
+case(
+    "hdiff_f64",
+    fields={
+        "in_field": fs(28, 24, 8),
+        "out_field": fs(24, 20, 8, init="zeros"),
+        "coeff": fs(24, 20, 8, init=("u", 0.0, 0.5)),
+    },
+    origin=_HD_ORIGIN,
+    domain=(24, 20, 8),
+    features=("hot",),
+)(hdiff_f64)
+case(
+    "hdiff_f64_demo",
+    fields={
+        "in_field": fs(36, 36, 6, init="demo"),
+        "out_field": fs(32, 32, 6, init="zeros"),
+        "coeff": fs(32, 32, 6, init=("const", 0.025)),
+    },
+    origin=_HD_ORIGIN,
+    domain=(32, 32, 6),
+    features=("hot",),
+)(hdiff_f64)
+case(
+    "hdiff_f64_origin",
+    fields={
+        "in_field": fs(30, 27, 10),
+        "out_field": fs(30, 27, 10),
+        "coeff": fs(30, 27, 10, init=("u", 0.0, 0.5)),
+    },
+    origin=(3, 2, 1),
+    domain=(21, 19, 7),
+    features=("hot",),
+)(hdiff_f64)
+case(
+    "hdiff_f64_ties",  # integer-valued inputs hit exact res*du == 0 limiter ties
+    fields={
+        "in_field": fs(20, 18, 4, init=("int", -3, 4)),
+        "out_field": fs(16, 14, 4, init="zeros"),
+        "coeff": fs(16, 14, 4, init=("int", 0, 2)),
+    },
+    origin=_HD_ORIGIN,
+    domain=(16, 14, 4),
+    features=("hot",),
+)(hdiff_f64)
+case(
+    "hdiff_f64_nan",  # NaN/Inf propagation (numpy runs under errstate(ignore))
+    fields={
+        "in_field": fs(20, 18, 4, nan_frac=0.01),
+        "out_field": fs(16, 14, 4, init="zeros"),
+        "coeff": fs(16, 14, 4, init=("u", 0.0, 0.5)),
+    },
+    origin=_HD_ORIGIN,
+    domain=(16, 14, 4),
+    features=("hot",),
+)(hdiff_f64)
+case(
+    "hdiff_f32",
+    fields={
+        "in_field": fs(28, 24, 8, dtype="f4"),
+        "out_field": fs(24, 20, 8, dtype="f4", init="zeros"),
+        "coeff": fs(24, 20, 8, dtype="f4", init=("u", 0.0, 0.5)),
+    },
+    origin=_HD_ORIGIN,
+    domain=(24, 20, 8),
+    features=("hot",),
+)(hdiff_f32)
+case(
+    "hdiff_f32_demo",
+    fields={
+        "in_field": fs(36, 36, 6, dtype="f4", init="demo"),
+        "out_field": fs(32, 32, 6, dtype="f4", init="zeros"),
+        "coeff": fs(32, 32, 6, dtype="f4", init=("const", 0.025)),
+    },
+    origin=_HD_ORIGIN,
+    domain=(32, 32, 6),
+    features=("hot",),
+)(hdiff_f32)
+
+
+def tridiagonal_solver(inf: F64, diag: F64, sup: F64, rhs: F64, out: F64):
+    with computation(FORWARD):
+        with interval(0, 1):
+            sup = sup / diag
+            rhs = rhs / diag
+        with interval(1, None):
+            sup = sup / (diag - sup[0, 0, -1] * inf)
+            rhs = (rhs - inf * rhs[0, 0, -1]) / (diag - sup[0, 0, -1] * inf)
+    with computation(BACKWARD):
+        with interval(-1, None):
+            out = rhs
+        with interval(0, -1):
+            out = rhs - sup * out[0, 0, 1]
+
+
+def _tridiag_fields(ni, nj, nk):
+    return {
+        "inf": fs(ni, nj, nk, init=("u", -1.0, 1.0)),
+        "diag": fs(ni, nj, nk, init=("u", 4.0, 5.0)),
+        "sup": fs(ni, nj, nk, init=("u", -1.0, 1.0)),
+        "rhs": fs(ni, nj, nk, init=("u", -10.0, 10.0)),
+        "out": fs(ni, nj, nk, init="zeros"),
+    }
+
+
+case("tridiag", fields=_tridiag_fields(8, 6, 32), features=("hot",))(tridiagonal_solver)
+case("tridiag_k2", fields=_tridiag_fields(5, 4, 2), features=("hot",))(tridiagonal_solver)
+case(
+    "tridiag_subdomain",
+    fields=_tridiag_fields(9, 7, 12),
+    origin=(1, 2, 1),
+    domain=(7, 4, 9),
+    features=("hot",),
+)(tridiagonal_solver)
+
+
+# --------------------------------------------------------------------------------------
+# test_suites.py programs
+# --------------------------------------------------------------------------------------
+
+
+def suite_identity(field_a: F64):
+    with computation(PARALLEL), interval(...):
+        tmp = field_a
+        field_a = tmp
+
+
+case("suite_identity", fields={"field_a": fs(9, 7, 5)})(suite_identity)
+
+
+def suite_aug_assign(field_a: F64, field_b: F64):
+    with computation(PARALLEL), interval(...):
+        field_a += 1.0
+        field_a *= 2.0
+        field_b -= 1.0
+        field_b /= 2.0
+
+
+case("suite_aug_assign", fields={"field_a": fs(9, 7, 5), "field_b": fs(9, 7, 5)})(suite_aug_assign)
+
+
+def suite_global_scale(field_a: F64):
+    from __externals__ import SCALE_FACTOR
+
+    with computation(PARALLEL), interval(...):
+        field_a = SCALE_FACTOR * field_a[0, 0, 0]
+
+
+case("suite_global_scale", fields={"field_a": fs(8, 6, 5, init=("u", -1.0, 1.0))}, externals={"SCALE_FACTOR": 1e3})(
+    suite_global_scale
+)
+
+
+def suite_parametric_scale(field_a: F64, *, scale: float):
+    with computation(PARALLEL), interval(...):
+        field_a = scale * field_a
+
+
+case("suite_parametric_scale", fields={"field_a": fs(8, 6, 5)}, params={"scale": -37.25})(suite_parametric_scale)
+
+
+def suite_parametric_mix(
+    field_a: F64, field_b: F64, field_c: F64, field_out: F32, *, weight: np.float64, alpha_factor: np.float64
+):
+    from __externals__ import USE_ALPHA
+    from __gtscript__ import __INLINED
+
+    with computation(PARALLEL), interval(...):
+        if __INLINED(USE_ALPHA):
+            factor = alpha_factor
+        else:
+            factor = 1.0
+        field_out = factor * field_a[0, 0, 0] - (1 - factor) * (field_b[0, 0, 0] - weight * field_c[0, 0, 0])
+
+
+for _ua in (True, False):
+    case(
+        f"suite_parametric_mix_{int(_ua)}",
+        fields={
+            "field_a": fs(8, 7, 6),
+            "field_b": fs(8, 7, 6),
+            "field_c": fs(8, 7, 6),
+            "field_out": fs(8, 7, 6, dtype="f4"),
+        },
+        params={"weight": 3.5, "alpha_factor": -0.75},
+        externals={"USE_ALPHA": _ua},
+    )(suite_parametric_mix)
+
+
+def suite_heat_equation(u: F64, v: F64, u_new: F64, v_new: F64, *, ru: float, rv: float):
+    with computation(PARALLEL), interval(...):
+        u_new = u[0, 0, 0] + ru * (u[1, 0, 0] - 2 * u[0, 0, 0] + u[-1, 0, 0])
+        v_new = v[0, 0, 0] + rv * (v[0, 1, 0] - 2 * v[0, 0, 0] + v[0, -1, 0])
+
+
+case(
+    "suite_heat_equation",
+    fields={"u": fs(12, 9, 6), "v": fs(10, 11, 6), "u_new": fs(10, 9, 6), "v_new": fs(10, 9, 6)},
+    params={"ru": 0.3, "rv": 0.125},
+    origin={"u": (1, 0, 0), "v": (0, 1, 0), "u_new": (0, 0, 0), "v_new": (0, 0, 0)},
+    domain=(10, 9, 6),
+)(suite_heat_equation)
+
+
+def suite_hdiff_weight(u: F64, diffusion: F64, *, weight: float):
+    with computation(PARALLEL), interval(...):
+        laplacian = 4.0 * u[0, 0, 0] - (u[1, 0, 0] + u[-1, 0, 0] + u[0, 1, 0] + u[0, -1, 0])
+        flux_i = laplacian[1, 0, 0] - laplacian[0, 0, 0]
+        flux_j = laplacian[0, 1, 0] - laplacian[0, 0, 0]
+        diffusion = u[0, 0, 0] - weight * (flux_i[0, 0, 0] - flux_i[-1, 0, 0] + flux_j[0, 0, 0] - flux_j[0, -1, 0])
+
+
+case(
+    "suite_hdiff_weight",
+    fields={"u": fs(17, 15, 5), "diffusion": fs(13, 11, 5)},
+    params={"weight": 0.375},
+    origin={"u": (2, 2, 0), "diffusion": (0, 0, 0)},
+    domain=(13, 11, 5),
+)(suite_hdiff_weight)
+
+
+@gtscript.function
+def lap_op(u):
+    """Laplacian operator."""
+    return 4.0 * u[0, 0, 0] - (u[1, 0, 0] + u[-1, 0, 0] + u[0, 1, 0] + u[0, -1, 0])
+
+
+@gtscript.function
+def fwd_diff_op_xy(field):
+    dx = field[1, 0, 0] - field[0, 0, 0]
+    dy = field[0, 1, 0] - field[0, 0, 0]
+    return dx, dy
+
+
+@gtscript.function
+def wrap1arg2return(field):
+    dx, dy = fwd_diff_op_xy(field=field)
+    return dx, dy
+
+
+@gtscript.function
+def fwd_diff_op_x(field):
+    dx = field[1, 0, 0] - field[0, 0, 0]
+    return dx
+
+
+@gtscript.function
+def fwd_diff_op_y(field):
+    dy = field[0, 1, 0] - field[0, 0, 0]
+    return dy
+
+
+def suite_hdiff_subroutines(u: F64, diffusion: F64, *, weight: float):
+    from __externals__ import fwd_diff
+
+    with computation(PARALLEL), interval(...):
+        laplacian = lap_op(u=u)
+        flux_i, flux_j = fwd_diff(field=laplacian)
+        diffusion = u[0, 0, 0] - weight * (flux_i[0, 0, 0] - flux_i[-1, 0, 0] + flux_j[0, 0, 0] - flux_j[0, -1, 0])
+
+
+case(
+    "suite_hdiff_subroutines",
+    fields={"u": fs(17, 15, 5), "diffusion": fs(13, 11, 5)},
+    params={"weight": 0.25},
+    externals={"fwd_diff": wrap1arg2return},
+    origin={"u": (2, 2, 0), "diffusion": (0, 0, 0)},
+    domain=(13, 11, 5),
+)(suite_hdiff_subroutines)
+
+
+def suite_hdiff_subroutines2(u: F64, diffusion: F64, *, weight: float):
+    from __externals__ import BRANCH
+    from __gtscript__ import __INLINED
+
+    with computation(PARALLEL), interval(...):
+        laplacian = lap_op(u=u)
+        if __INLINED(BRANCH):
+            flux_i = fwd_diff_op_x(field=laplacian)
+            flux_j = fwd_diff_op_y(field=laplacian)
+        else:
+            flux_i, flux_j = fwd_diff_op_xy(field=laplacian)
+        diffusion = u[0, 0, 0] - weight * (flux_i[0, 0, 0] - flux_i[-1, 0, 0] + flux_j[0, 0, 0] - flux_j[0, -1, 0])
+
+
+for _br in (True, False):
+    case(
+        f"suite_hdiff_subroutines2_{int(_br)}",
+        fields={"u": fs(17, 15, 5), "diffusion": fs(13, 11, 5)},
+        params={"weight": 0.125},
+        externals={"BRANCH": _br},
+        origin={"u": (2, 2, 0), "diffusion": (0, 0, 0)},
+        domain=(13, 11, 5),
+    )(suite_hdiff_subroutines2)
+
+
+def suite_runtime_if_flat(outfield: F64):
+    with computation(PARALLEL), interval(...):
+        if True:
+            outfield = 1
+        else:
+            outfield = 2
+
+
+case("suite_runtime_if_flat", fields={"outfield": fs(6, 5, 4)})(suite_runtime_if_flat)
+
+
+def suite_runtime_if_nested(outfield: F64):
+    with computation(PARALLEL), interval(...):
+        if (outfield > 0 and outfield > 0) or (not outfield > 0 and not outfield > 0):
+            if False:
+                outfield = 1
+            else:
+                outfield = 2
+        else:
+            outfield = 3
+
+
+case("suite_runtime_if_nested", fields={"outfield": fs(6, 5, 4)})(suite_runtime_if_nested)
+
+
+def suite_3fold_nested_if(field_a: F64):
+    with computation(PARALLEL), interval(...):
+        if field_a >= 0.0:
+            field_a = 0.0
+            if field_a > 1:
+                field_a = 1
+                if field_a > 2:
+                    field_a = 2
+
+
+case("suite_3fold_nested_if", fields={"field_a": fs(5, 5, 5, init=("u", -1.0, 1.0))})(suite_3fold_nested_if)
+
+
+@gtscript.function
+def add_one(field_in):
+    """Add 1 to each element of `field_in`."""
+    return field_in + 1
+
+
+def suite_runtime_if_data_dependent(field_a: F64, field_b: F64, field_c: F64, *, factor: float):
+    with computation(PARALLEL), interval(...):
+        if factor > 0:
+            if field_a < 0:
+                field_b = -field_a
+            else:
+                field_b = field_a
+        else:
+            if field_a < 0:
+                field_c = -field_a
+            else:
+                field_c = field_a
+        field_a = add_one(field_a)
+
+
+for _fac in (12.5, -3.0):
+    case(
+        f"suite_runtime_if_data_dependent_{'p' if _fac > 0 else 'm'}",
+        fields={"field_a": fs(5, 4, 3, init=("u", -1.0, 1.0)), "field_b": fs(5, 4, 3), "field_c": fs(5, 4, 3)},
+        params={"factor": _fac},
+    )(suite_runtime_if_data_dependent)
+
+
+def suite_runtime_if_nested_while(infield: F64, outfield: F64):
+    with computation(PARALLEL), interval(...):
+        if infield < 10:
+            outfield = 1
+            done = False
+            while not done:
+                outfield = 2
+                done = True
+        else:
+            condition = True
+            while condition:
+                outfield = 4
+                condition = False
+            outfield = 3
+
+
+case(
+    "suite_runtime_if_nested_while",
+    fields={"infield": fs(6, 5, 4, init=("u", -20.0, 20.0)), "outfield": fs(6, 5, 4)},
+)(suite_runtime_if_nested_while)
+
+
+def suite_ternary_op(infield: F64, outfield: F64):
+    with computation(PARALLEL), interval(...):
+        outfield = infield if infield > 0.0 else -infield[0, 1, 0]
+
+
+case(
+    "suite_ternary_op",
+    fields={"infield": fs(7, 9, 4), "outfield": fs(7, 8, 4)},
+    domain=(7, 8, 4),
+)(suite_ternary_op)
+
+
+def suite_three_way_and(outfield: F64, *, a: float, b: float, c: float):
+    with computation(PARALLEL), interval(...):
+        if a > 0 and b > 0 and c > 0:
+            outfield = 1
+        else:
+            outfield = 0
+
+
+def suite_three_way_or(outfield: F64, *, a: float, b: float, c: float):
+    with computation(PARALLEL), interval(...):
+        if a > 0 or b > 0 or c > 0:
+            outfield = 1
+        else:
+            outfield = 0
+
+
+case("suite_three_way_and", fields={"outfield": fs(4, 4, 3)}, params={"a": 1.0, "b": 2.0, "c": 3.0})(suite_three_way_and)
+case("suite_three_way_or", fields={"outfield": fs(4, 4, 3)}, params={"a": -1.0, "b": -2.0, "c": 3.0})(suite_three_way_or)
+
+
+def optional_field(in_field: F64, out_field: F64, dyn_tend: F64, phys_tend: F64 = None, *, dt: float):
+    from __externals__ import PHYS_TEND
+
+    with computation(PARALLEL), interval(...):
+        out_field = in_field + dt * dyn_tend
+        if __INLINED(PHYS_TEND):
+            out_field = out_field + dt * phys_tend
+
+
+case(
+    "optional_field_used",
+    fields={"in_field": fs(7, 6, 5), "out_field": fs(7, 6, 5), "dyn_tend": fs(7, 6, 5), "phys_tend": fs(7, 6, 5)},
+    params={"dt": 0.5},
+    externals={"PHYS_TEND": True},
+)(optional_field)
+case(
+    "optional_field_unused",
+    fields={"in_field": fs(7, 6, 5), "out_field": fs(7, 6, 5), "dyn_tend": fs(7, 6, 5), "phys_tend": None},
+    params={"dt": 0.5},
+    externals={"PHYS_TEND": False},
+)(optional_field)
+
+
+# --------------------------------------------------------------------------------------
+# stencil_definitions.py programs
+# --------------------------------------------------------------------------------------
+
+
+def arithmetic_ops(field_a: F64, field_b: F64):
+    with computation(PARALLEL), interval(...):
+        field_a = (((((field_b + 42.0) - 42.0) * +42.0) / -42.0) % 42.0) ** 2
+
+
+case("arithmetic_ops", fields={"field_a": fs(6, 5, 4), "field_b": fs(6, 5, 4)}, rtol=1e-14)(arithmetic_ops)
+
+
+def scalar_inputs(field_a: F64, scalar_in: float):
+    with computation(PARALLEL), interval(...):
+        field_a = field_a * scalar_in
+
+
+case("scalar_inputs", fields={"field_a": fs(6, 5, 4)}, params={"scalar_in": 1.5})(scalar_inputs)
+
+
+def unary_operation(field_a: F64, scalar_in: float):
+    with computation(PARALLEL), interval(...):
+        field_a = -scalar_in
+
+
+case("unary_operation", fields={"field_a": fs(6, 5, 4)}, params={"scalar_in": 2.75})(unary_operation)
+
+
+def temporary_stencil(field_a: F64, field_b: F2D, scalar_in: float):
+    with computation(PARALLEL), interval(...):
+        tmp = field_a * scalar_in
+
+    with computation(FORWARD), interval(0, 1):
+        field_b += tmp
+
+
+case(
+    "temporary_stencil",
+    fields={"field_a": fs(6, 5, 4), "field_b": fs(6, 5)},
+    params={"scalar_in": 3.0},
+    features=("2d",),
+)(temporary_stencil)
+
+
+@gtscript.function
+def a_gtscript_function(b):
+    return sqrt(abs(b[0, 1, 0]))
+
+
+def native_functions(field_a: F64, field_b: F64):
+    with computation(PARALLEL), interval(...):
+        abs_res = abs(field_a)
+        max_res = max(abs_res, 1.0)
+        min_res = min(max_res, 42)
+        mod_res = mod(min_res, 37.5)
+        sin_res = sin(mod_res)
+        asin_res = asin(sin_res)
+        cos_res = cos(asin_res)
+        acos_res = acos(cos_res)
+        tan_res = tan(acos_res)
+        atan_res = atan(tan_res)
+        sinh_res = sinh(atan_res)
+        asinh_res = asinh(sinh_res)
+        cosh_res = cosh(asinh_res)
+        acosh_res = acosh(cosh_res)
+        tanh_res = tanh(acosh_res)
+        atanh_res = atanh(tanh_res)
+        sqrt_res = a_gtscript_function(atanh_res)
+        pow10_res = 10 ** (sqrt_res)
+        log10_res = log10(pow10_res)
+        exp_res = exp(log10_res)
+        log_res = log(exp_res)
+        gamma_res = gamma(log_res)
+        cbrt_res = cbrt(gamma_res)
+        floor_res = floor(cbrt_res)
+        ceil_res = ceil(floor_res)
+        trunc_res = trunc(ceil_res)
+        round_res = round(trunc_res)
+        round_afz_res = round_away_from_zero(round_res)
+        erf_res = erf(round_afz_res)
+        erfc_res = erfc(erf_res)
+        field_b = (
+            trunc_res
+            if isfinite(erfc_res)
+            else field_a
+            if isinf(erfc_res)
+            else field_b
+            if isnan(erfc_res)
+            else 0.0
+        )
+
+
+case(
+    "native_functions",
+    fields={"field_a": fs(6, 6, 4), "field_b": fs(6, 5, 4)},
+    domain=(6, 5, 4),
+    rtol=1e-12,
+    atol=1e-12,
+)(native_functions)
+
+
+def math_chain(field_a: F64, field_b: F64):
+    with computation(PARALLEL), interval(...):
+        field_b = sqrt(abs(field_a)) + exp(field_a * 0.1) - log(abs(field_a) + 1.0) + sin(field_a) * cos(field_a)
+
+
+case("math_chain", fields={"field_a": fs(8, 6, 4), "field_b": fs(8, 6, 4)}, rtol=1e-13, atol=1e-13)(math_chain)
+
+
+def while_stencil(field_a: F64, field_b: F64):
+    with computation(BACKWARD), interval(...):
+        while field_a > 2.0:
+            field_b = -1
+            field_a = -field_b
+
+
+case("while_stencil", fields={"field_a": fs(6, 5, 4), "field_b": fs(6, 5, 4)})(while_stencil)
+
+
+def copy_stencil_plus_one(field_a: F64, field_b: F64):
+    with computation(PARALLEL), interval(...):
+        field_b = field_a[0, 0, 0] + 1
+
+
+case("copy_stencil_plus_one", fields={"field_a": fs(6, 5, 4), "field_b": fs(6, 5, 4)})(copy_stencil_plus_one)
+
+
+def runtime_if(field_a: F64, field_b: F64):
+    with computation(BACKWARD), interval(...):
+        if field_a > 0.0:
+            field_b = -1
+            field_a = -field_a
+        else:
+            field_b = 1
+            field_a = field_a
+
+
+case("runtime_if", fields={"field_a": fs(6, 5, 4), "field_b": fs(6, 5, 4)})(runtime_if)
+
+
+def simple_horizontal_diffusion(in_field: F64, coeff: F64, out_field: F64):
+    with computation(PARALLEL), interval(...):
+        lap_field = 4.0 * in_field[0, 0, 0] - (
+            in_field[1, 0, 0] + in_field[-1, 0, 0] + in_field[0, 1, 0] + in_field[0, -1, 0]
+        )
+        flx_field = lap_field[1, 0, 0] - lap_field[0, 0, 0]
+        fly_field = lap_field[0, 1, 0] - lap_field[0, 0, 0]
+        out_field = in_field[0, 0, 0] - coeff[0, 0, 0] * (
+            flx_field[0, 0, 0] - flx_field[-1, 0, 0] + fly_field[0, 0, 0] - fly_field[0, -1, 0]
+        )
+
+
+case(
+    "simple_horizontal_diffusion",
+    fields={"in_field": fs(16, 14, 5), "coeff": fs(12, 10, 5, init=("u", 0.0, 0.5)), "out_field": fs(12, 10, 5)},
+    origin={"in_field": (2, 2, 0), "coeff": (0, 0, 0), "out_field": (0, 0, 0)},
+    domain=(12, 10, 5),
+)(simple_horizontal_diffusion)
+
+
+def vertical_advection_dycore(
+    utens_stage: F64,
+    u_stage: F64,
+    wcon: F64,
+    u_pos: F64,
+    utens: F64,
+    *,
+    dtr_stage: float,
+):
+    from __externals__ import BET_M, BET_P
+
+    with computation(FORWARD):
+        with interval(0, 1):
+            gcv = 0.25 * (wcon[1, 0, 1] + wcon[0, 0, 1])
+            cs = gcv * BET_M
+
+            ccol = gcv * BET_P
+            bcol = dtr_stage - ccol[0, 0, 0]
+
+            correction_term = -cs * (u_stage[0, 0, 1] - u_stage[0, 0, 0])
+            dcol = dtr_stage * u_pos[0, 0, 0] + utens[0, 0, 0] + utens_stage[0, 0, 0] + correction_term
+
+            divided = 1.0 / bcol[0, 0, 0]
+            ccol = ccol[0, 0, 0] * divided
+            dcol = dcol[0, 0, 0] * divided
+
+        with interval(1, -1):
+            gav = -0.25 * (wcon[1, 0, 0] + wcon[0, 0, 0])
+            gcv = 0.25 * (wcon[1, 0, 1] + wcon[0, 0, 1])
+
+            as_ = gav * BET_M
+            cs = gcv * BET_M
+
+            acol = gav * BET_P
+            ccol = gcv * BET_P
+            bcol = dtr_stage - acol[0, 0, 0] - ccol[0, 0, 0]
+
+            correction_term = -as_ * (u_stage[0, 0, -1] - u_stage[0, 0, 0]) - cs * (
+                u_stage[0, 0, 1] - u_stage[0, 0, 0]
+            )
+            dcol = dtr_stage * u_pos[0, 0, 0] + utens[0, 0, 0] + utens_stage[0, 0, 0] + correction_term
+
+            divided = 1.0 / (bcol[0, 0, 0] - ccol[0, 0, -1] * acol[0, 0, 0])
+            ccol = ccol[0, 0, 0] * divided
+            dcol = (dcol[0, 0, 0] - (dcol[0, 0, -1]) * acol[0, 0, 0]) * divided
+
+        with interval(-1, None):
+            gav = -0.25 * (wcon[1, 0, 0] + wcon[0, 0, 0])
+            as_ = gav * BET_M
+            acol = gav * BET_P
+            bcol = dtr_stage - acol[0, 0, 0]
+
+            correction_term = -as_ * (u_stage[0, 0, -1] - u_stage[0, 0, 0])
+            dcol = dtr_stage * u_pos[0, 0, 0] + utens[0, 0, 0] + utens_stage[0, 0, 0] + correction_term
+
+            divided = 1.0 / (bcol[0, 0, 0] - ccol[0, 0, -1] * acol[0, 0, 0])
+            dcol = (dcol[0, 0, 0] - (dcol[0, 0, -1]) * acol[0, 0, 0]) * divided
+
+    with computation(BACKWARD):
+        with interval(-1, None):
+            datacol = dcol[0, 0, 0]
+            utens_stage = dtr_stage * (datacol - u_pos[0, 0, 0])
+
+        with interval(0, -1):
+            datacol = dcol[0, 0, 0] - ccol[0, 0, 0] * datacol[0, 0, 1]
+            utens_stage = dtr_stage * (datacol - u_pos[0, 0, 0])
+
+
+case(
+    "vertical_advection_dycore",
+    fields={
+        "utens_stage": fs(8, 7, 10),
+        "u_stage": fs(8, 7, 10),
+        "wcon": fs(9, 7, 11, init=("u", -1.0, 1.0)),
+        "u_pos": fs(8, 7, 10),
+        "utens": fs(8, 7, 10),
+    },
+    params={"dtr_stage": 3.0 / 20.0},
+    externals={"BET_M": 0.5, "BET_P": 0.5},
+    domain=(8, 7, 10),
+    rtol=1e-13,
+    atol=1e-13,
+)(vertical_advection_dycore)
+
+
+def large_k_interval(in_field: F64, out_field: F64):
+    with computation(PARALLEL):
+        with interval(0, 6):
+            out_field = in_field
+        with interval(6, -10):
+            out_field = in_field + 1
+        with interval(-10, None):
+            out_field = in_field
+
+
+case("large_k_interval", fields={"in_field": fs(5, 4, 20), "out_field": fs(5, 4, 20)})(large_k_interval)
+
+
+def single_level_with_offset(in_field: F64, out_field: F64):
+    with computation(PARALLEL), interval(1, 2):
+        out_field = in_field
+
+
+case("single_level_with_offset", fields={"in_field": fs(5, 4, 6), "out_field": fs(5, 4, 6)})(single_level_with_offset)
+
+
+def form_land_mask(in_field: F64, mask: FBool):
+    with computation(PARALLEL), interval(...):
+        mask = in_field >= 0
+
+
+case("form_land_mask", fields={"in_field": fs(6, 5, 4), "mask": fs(6, 5, 4, dtype="?", init="bool")})(form_land_mask)
+
+
+def set_inner_as_kord(a4_1: F64, a4_2: F64, a4_3: F64, extm: FBool):
+    with computation(PARALLEL), interval(...):
+        diff_23 = 0.0
+        if extm and extm[0, 0, -1]:
+            a4_2 = a4_1
+        elif extm and extm[0, 0, 1]:
+            a4_3 = a4_1
+        else:
+            diff_23 = a4_2 - a4_3
+
+
+case(
+    "set_inner_as_kord",
+    fields={"a4_1": fs(6, 5, 8), "a4_2": fs(6, 5, 8), "a4_3": fs(6, 5, 8), "extm": fs(6, 5, 10, dtype="?", init="bool")},
+    origin={"a4_1": (0, 0, 0), "a4_2": (0, 0, 0), "a4_3": (0, 0, 0), "extm": (0, 0, 1)},
+    domain=(6, 5, 8),
+)(set_inner_as_kord)
+
+
+def local_var_inside_nested_conditional(in_storage: F64, out_storage: F64):
+    with computation(PARALLEL), interval(0, 2):
+        mid_storage = 2
+        if in_storage[0, 0, 0] > 0:
+            local_var = 4
+            if local_var + in_storage < out_storage:
+                mid_storage = 3
+            else:
+                mid_storage = 4
+            out_storage[0, 0, 0] = local_var + mid_storage
+    with computation(FORWARD), interval(2, None):
+        if in_storage[0, 0, 0] < 0:
+            local_var = 6
+            out_storage[0, 0, 0] = local_var
+
+
+case(
+    "local_var_inside_nested_conditional",
+    fields={"in_storage": fs(6, 5, 6), "out_storage": fs(6, 5, 6)},
+)(local_var_inside_nested_conditional)
+
+
+def multibranch_param_conditional(in_field: F64, out_field: F64, c: float):
+    with computation(PARALLEL), interval(...):
+        if c > 0.0:
+            out_field = in_field + in_field[1, 0, 0]
+        elif c < -1.0:
+            out_field = in_field - in_field[1, 0, 0]
+        else:
+            out_field = in_field
+
+
+for _c, _tag in ((1.0, "pos"), (-2.0, "neg"), (-0.5, "mid")):
+    case(
+        f"multibranch_param_conditional_{_tag}",
+        fields={"in_field": fs(7, 5, 4), "out_field": fs(6, 5, 4)},
+        params={"c": _c},
+        domain=(6, 5, 4),
+    )(multibranch_param_conditional)
+
+
+def allow_empty_computation(in_field: F64, out_field: F64):
+    from __externals__ import DO_SOMETHING
+
+    with computation(FORWARD), interval(...):
+        out_field = in_field
+    with computation(PARALLEL), interval(...):
+        if __INLINED(DO_SOMETHING):
+            out_field = abs(in_field)
+
+
+case(
+    "allow_empty_computation",
+    fields={"in_field": fs(6, 5, 4), "out_field": fs(6, 5, 4)},
+    externals={"DO_SOMETHING": False},
+)(allow_empty_computation)
+
+
+def two_optional_fields(
+    in_a: F64,
+    in_b: F64,
+    out_a: F64,
+    out_b: F64,
+    dyn_tend_a: F64,
+    dyn_tend_b: F64,
+    phys_tend_a: F64 = None,
+    phys_tend_b: F64 = None,
+    *,
+    dt: float,
+):
+    from __externals__ import PHYS_TEND_A, PHYS_TEND_B
+
+    with computation(PARALLEL), interval(...):
+        out_a = in_a + dt * dyn_tend_a
+        out_b = in_b + dt * dyn_tend_b
+        if __INLINED(PHYS_TEND_A):
+            out_a = out_a + dt * phys_tend_a
+        if __INLINED(PHYS_TEND_B):
+            out_b = out_b + dt * phys_tend_b
+
+
+for _pa, _pb in ((False, False), (False, True), (True, True)):
+    case(
+        f"two_optional_fields_{int(_pa)}{int(_pb)}",
+        fields={
+            "in_a": fs(5, 4, 3),
+            "in_b": fs(5, 4, 3),
+            "out_a": fs(5, 4, 3),
+            "out_b": fs(5, 4, 3),
+            "dyn_tend_a": fs(5, 4, 3),
+            "dyn_tend_b": fs(5, 4, 3),
+            "phys_tend_a": fs(5, 4, 3) if _pa else None,
+            "phys_tend_b": fs(5, 4, 3) if _pb else None,
+        },
+        params={"dt": 0.25},
+        externals={"PHYS_TEND_A": _pa, "PHYS_TEND_B": _pb},
+    )(two_optional_fields)
+
+
+def horizontal_regions(field_in: F64, field_out: F64):
+    with computation(PARALLEL), interval(...):
+        with horizontal(region[I[0] : I[0] + 2, J[0] : J[0] + 2], region[I[-1] - 2 : I[-1], J[-1] - 2 : J[-1]]):
+            field_out = field_in + 1.0
+
+        with horizontal(region[I[0] : I[0] + 2, J[-1] - 2 : J[-1]], region[I[-1] - 2 : I[-1], J[0] : J[0] + 2]):
+            field_out = field_in - 1.0
+
+
+case(
+    "horizontal_regions",
+    fields={"field_in": fs(8, 7, 3), "field_out": fs(8, 7, 3)},
+    features=("regions",),
+)(horizontal_regions)
+
+
+def mixed_precision(a: F32, b: F64, out32: F32, out64: F64):
+    with computation(PARALLEL), interval(...):
+        t32 = a + 1
+        t64 = a * 2.0 + b
+        out32 = t32 * a - b
+        out64 = t64 / (a + 3) + t32
+
+
+case(
+    "mixed_precision",
+    fields={"a": fs(7, 6, 5, dtype="f4"), "b": fs(7, 6, 5), "out32": fs(7, 6, 5, dtype="f4"), "out64": fs(7, 6, 5)},
+)(mixed_precision)
+
+
+def kcache_forward_backward(a: F64, b: F64, c: F64):
+    with computation(FORWARD):
+        with interval(0, 1):
+            tmp = a
+            b = tmp
+        with interval(1, None):
+            tmp = a + 0.5 * tmp[0, 0, -1]
+            b = tmp * b[0, 0, -1]
+    with computation(BACKWARD):
+        with interval(-1, None):
+            c = tmp
+        with interval(0, -1):
+            c = tmp - 0.25 * c[0, 0, 1] + a[0, 0, 1]
+
+
+case(
+    "kcache_forward_backward",
+    fields={"a": fs(6, 5, 9, init=("u", -1.0, 1.0)), "b": fs(6, 5, 9, init=("u", -1.0, 1.0)), "c": fs(6, 5, 9)},
+)(kcache_forward_backward)
+
+
+def parallel_koffsets(a: F64, b: F64):
+    with computation(PARALLEL):
+        with interval(0, 1):
+            b = a[0, 0, 1] - a
+        with interval(1, -1):
+            b = a[0, 0, 1] - 2.0 * a + a[0, 0, -1]
+        with interval(-1, None):
+            b = a[0, 0, -1] - a
+
+
+case("parallel_koffsets", fields={"a": fs(6, 5, 7), "b": fs(6, 5, 7)})(parallel_koffsets)
+
+
+def multi_stage_temps(a: F64, out: F64, *, alpha: float):
+    with computation(PARALLEL), interval(...):
+        t1 = a[1, 0, 0] - a[-1, 0, 0]
+        t2 = a[0, 1, 0] - a[0, -1, 0]
+        t3 = t1[0, 1, 0] + t2[1, 0, 0] + alpha * t1[0, -1, 0] * t2[-1, 0, 0]
+        out = t3[1, 1, 0] - t3[-1, -1, 0] + t3
+
+
+case(
+    "multi_stage_temps",
+    fields={"a": fs(15, 13, 4), "out": fs(11, 9, 4)},
+    params={"alpha": 0.5},
+    origin={"a": (2, 2, 0), "out": (0, 0, 0)},
+    domain=(11, 9, 4),
+)(multi_stage_temps)
