@@ -1,0 +1,171 @@
+"""Kernel planning for gt:mi355x.
+
+Splits a typed stencil (``passes.StencilAnalysis``) into HIP launches of two hand-written
+execution patterns (SURVEY.md §2.1 N1 -> K1/K2):
+
+- ``PlaneKernel`` (K1): one PARALLEL interval section that has horizontal offsets. Lowered to
+  the J-streaming skeleton: a wavefront owns a 64-wide I strip and walks a chunk of J rows at
+  one K level; every value (field load, temporary version) lives in a register ring of the
+  depth its J offsets need, and I offsets are wave shuffles. No LDS, no barriers.
+- ``ColumnKernel`` (K2): a run of vertical loops without horizontal offsets on values produced
+  inside the run (FORWARD/BACKWARD sweeps, and PARALLEL loops that are pointwise in IJ). One
+  thread per (i, j) column walks the K levels in loop order with a register K-window per
+  accessed (name, di, dj) -- the register-carried K-cache of the reference's
+  ``KCacheDetection`` (``gtc/passes/oir_optimizations/caches.py:92``).
+
+Temporaries used by more than one launch (or by more than one vertical loop of a column
+kernel) become global *scratch* fields (I-first, allocated per domain by the host); all other
+temporaries live in registers only.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional, Set, Tuple
+
+from gt4py_amd import ir
+from gt4py_amd.passes import ZERO_EXTENT, StencilAnalysis, iter_accesses
+
+
+class UnsupportedStencil(NotImplementedError):
+    pass
+
+
+@dataclasses.dataclass
+class PlaneKernel:
+    loop: int
+    section: int
+
+    @property
+    def items(self):
+        return [(self.loop, self.section)]
+
+
+@dataclasses.dataclass
+class ColumnKernel:
+    loops: List[int]
+
+    def items(self, stencil):
+        return [(li, si) for li in self.loops for si in range(len(stencil.vertical_loops[li].sections))]
+
+
+@dataclasses.dataclass
+class KernelPlan:
+    kernels: List[object]
+    scratch: List[str]  # temporaries materialised in global memory
+    scratch_extent: Dict[str, Tuple[Tuple[int, int], Tuple[int, int]]]
+
+
+def _loop_accesses(vl: ir.VerticalLoop):
+    for sec in vl.sections:
+        yield from iter_accesses(sec.body)
+
+
+def _has_horizontal_offsets(vl: ir.VerticalLoop) -> bool:
+    for acc, _ in _loop_accesses(vl):
+        if isinstance(acc, ir.FieldAccess) and (acc.offset[0] != 0 or acc.offset[1] != 0):
+            return True
+    for sec in vl.sections:
+        for n in ir.walk(sec.body):
+            if isinstance(n, ir.HorizontalRegion):
+                return True
+    return False
+
+
+def make_plan(analysis: StencilAnalysis) -> KernelPlan:
+    st = analysis.stencil
+    temps = {t.name for t in st.temporaries}
+    api = {p.name for p in st.field_params()}
+
+    kernels: List[object] = []
+    run: List[int] = []
+
+    def flush():
+        if run:
+            kernels.append(ColumnKernel(list(run)))
+            run.clear()
+
+    for li, vl in enumerate(st.vertical_loops):
+        if vl.loop_order == ir.LoopOrder.PARALLEL and _has_horizontal_offsets(vl):
+            flush()
+            for si in range(len(vl.sections)):
+                kernels.append(PlaneKernel(li, si))
+        else:
+            if vl.loop_order != ir.LoopOrder.PARALLEL:
+                # sequential loops: values produced in the loop may not be read at IJ offsets
+                written = set()
+                for acc, w in _loop_accesses(vl):
+                    if w:
+                        written.add(acc.name)
+                for acc, w in _loop_accesses(vl):
+                    if (
+                        not w
+                        and isinstance(acc, ir.FieldAccess)
+                        and acc.name in written
+                        and (acc.offset[0] or acc.offset[1])
+                    ):
+                        raise UnsupportedStencil(
+                            f"'{acc.name}' is written in a {vl.loop_order.name} loop and read at a horizontal "
+                            f"offset {acc.offset[:2]} in the same loop"
+                        )
+            run.append(li)
+            # a column kernel may not consume temporaries at IJ offsets produced in the same run
+    flush()
+
+    # which kernel(s) / loops touch each temporary
+    touch_kernels: Dict[str, Set[int]] = {}
+    touch_loops: Dict[str, Set[int]] = {}
+    read_ij_offset: Set[str] = set()
+    for ki, k in enumerate(kernels):
+        loops = [k.loop] if isinstance(k, PlaneKernel) else k.loops
+        for li in loops:
+            vl = st.vertical_loops[li]
+            secs = [vl.sections[k.section]] if isinstance(k, PlaneKernel) else vl.sections
+            for sec in secs:
+                for acc, _ in iter_accesses(sec.body):
+                    if isinstance(acc, ir.FieldAccess) and acc.name in temps:
+                        touch_kernels.setdefault(acc.name, set()).add(ki)
+                        touch_loops.setdefault(acc.name, set()).add(li)
+                        if acc.offset[0] or acc.offset[1]:
+                            read_ij_offset.add(acc.name)
+    scratch = []
+    for t in st.temporaries:
+        kk = touch_kernels.get(t.name, set())
+        ll = touch_loops.get(t.name, set())
+        if len(kk) > 1 or len(ll) > 1:
+            scratch.append(t.name)
+    # column kernels must not read scratch temporaries written inside the same kernel at IJ offsets
+    for k in kernels:
+        if isinstance(k, ColumnKernel):
+            written = set()
+            for li in k.loops:
+                for acc, w in _loop_accesses(st.vertical_loops[li]):
+                    if w:
+                        written.add(acc.name)
+            for li in k.loops:
+                for acc, w in _loop_accesses(st.vertical_loops[li]):
+                    if (
+                        not w
+                        and isinstance(acc, ir.FieldAccess)
+                        and acc.name in written
+                        and (acc.offset[0] or acc.offset[1])
+                    ):
+                        raise UnsupportedStencil(
+                            f"'{acc.name}' is produced and read at an IJ offset inside one column kernel"
+                        )
+    # PARALLEL plane kernels: K offsets only on values not written in the same section
+    for k in kernels:
+        if isinstance(k, PlaneKernel):
+            sec = st.vertical_loops[k.loop].sections[k.section]
+            written = set()
+            for acc, w in iter_accesses(sec.body):
+                if w:
+                    written.add(acc.name)
+            for acc, w in iter_accesses(sec.body):
+                if not w and isinstance(acc, ir.FieldAccess) and acc.offset[2] and acc.name in written:
+                    raise UnsupportedStencil(
+                        f"'{acc.name}' is written in a PARALLEL section and read at a K offset in the same section"
+                    )
+    scratch_extent = {t: analysis.extents.fields.get(t, ZERO_EXTENT) for t in scratch}
+    del api
+    return KernelPlan(kernels, scratch, scratch_extent)

@@ -1,0 +1,115 @@
+// gtmi_device.h -- device-side helpers shared by every generated gt:mi355x stencil.
+//
+// Numerics follow the reference numpy backend (gtc/ufuncs.py + numpy's own loops):
+//  * min/max propagate NaN like np.minimum / np.maximum,
+//  * mod is np.remainder (npy_divmod: result takes the sign of the divisor),
+//  * round is np.round (half to even = rint), round_away_from_zero is
+//    copysign(floor(|x| + 0.5), x) (gtc/ufuncs.py:31-33),
+//  * integer power / remainder follow numpy's integer loops.
+// Everything is compiled with -ffp-contract=off so no FMA contraction changes rounding.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GTMI_DEV __device__ __forceinline__
+
+namespace gtmi {
+
+// ---------------------------------------------------------------- wave shuffles (wave64)
+// Value of `v` held by lane (lane_id + delta) mod 64. Executed by all lanes of the wave
+// (callers hoist shuffles out of divergent control flow).
+GTMI_DEV double shfl(double v, int delta) {
+    const int src = (int)(__lane_id() + delta) & 63;
+    return __shfl(v, src, 64);
+}
+GTMI_DEV float shfl(float v, int delta) {
+    const int src = (int)(__lane_id() + delta) & 63;
+    return __shfl(v, src, 64);
+}
+GTMI_DEV int64_t shfl(int64_t v, int delta) {
+    const int src = (int)(__lane_id() + delta) & 63;
+    return (int64_t)__shfl((long long)v, src, 64);
+}
+GTMI_DEV int32_t shfl(int32_t v, int delta) {
+    const int src = (int)(__lane_id() + delta) & 63;
+    return __shfl((int)v, src, 64);
+}
+GTMI_DEV int16_t shfl(int16_t v, int delta) { return (int16_t)shfl((int32_t)v, delta); }
+GTMI_DEV int8_t shfl(int8_t v, int delta) { return (int8_t)shfl((int32_t)v, delta); }
+GTMI_DEV bool shfl(bool v, int delta) { return shfl((int32_t)v, delta) != 0; }
+
+// ---------------------------------------------------------------- clamps
+GTMI_DEV int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// ---------------------------------------------------------------- math (numpy semantics)
+template <typename T> GTMI_DEV bool isnan_(T) { return false; }
+template <> GTMI_DEV bool isnan_<double>(double x) { return __builtin_isnan(x); }
+template <> GTMI_DEV bool isnan_<float>(float x) { return __builtin_isnan(x); }
+
+template <typename T> GTMI_DEV T minimum(T a, T b) {
+    if (isnan_(a)) return a;
+    if (isnan_(b)) return b;
+    return a < b ? a : b;
+}
+template <typename T> GTMI_DEV T maximum(T a, T b) {
+    if (isnan_(a)) return a;
+    if (isnan_(b)) return b;
+    return a > b ? a : b;
+}
+
+GTMI_DEV double absolute(double x) { return fabs(x); }
+GTMI_DEV float absolute(float x) { return fabsf(x); }
+GTMI_DEV int64_t absolute(int64_t x) { return x < 0 ? -x : x; }
+GTMI_DEV int32_t absolute(int32_t x) { return x < 0 ? -x : x; }
+GTMI_DEV int16_t absolute(int16_t x) { return (int16_t)(x < 0 ? -x : x); }
+GTMI_DEV int8_t absolute(int8_t x) { return (int8_t)(x < 0 ? -x : x); }
+GTMI_DEV bool absolute(bool x) { return x; }
+
+GTMI_DEV double remainder_(double a, double b) {
+    double mod = fmod(a, b);
+    if (b == 0.0) return mod;
+    if (mod != 0.0) {
+        if ((b < 0) != (mod < 0)) mod += b;
+    } else {
+        mod = copysign(0.0, b);
+    }
+    return mod;
+}
+GTMI_DEV float remainder_(float a, float b) {
+    float mod = fmodf(a, b);
+    if (b == 0.0f) return mod;
+    if (mod != 0.0f) {
+        if ((b < 0) != (mod < 0)) mod += b;
+    } else {
+        mod = copysignf(0.0f, b);
+    }
+    return mod;
+}
+template <typename T> GTMI_DEV T remainder_int(T a, T b) {
+    if (b == 0) return 0;
+    T r = a % b;
+    if (r != 0 && ((r < 0) != (b < 0))) r += b;
+    return r;
+}
+GTMI_DEV int64_t remainder_(int64_t a, int64_t b) { return remainder_int(a, b); }
+GTMI_DEV int32_t remainder_(int32_t a, int32_t b) { return remainder_int(a, b); }
+GTMI_DEV int16_t remainder_(int16_t a, int16_t b) { return remainder_int(a, b); }
+GTMI_DEV int8_t remainder_(int8_t a, int8_t b) { return remainder_int(a, b); }
+
+template <typename T> GTMI_DEV T ipow(T base, T exp) {
+    if (exp < 0) return (T)0;  // numpy raises; keep it defined on device
+    T r = 1;
+    while (exp) {
+        if (exp & 1) r *= base;
+        base *= base;
+        exp >>= 1;
+    }
+    return r;
+}
+
+GTMI_DEV double round_half_even(double x) { return rint(x); }
+GTMI_DEV float round_half_even(float x) { return rintf(x); }
+GTMI_DEV double round_away(double x) { return copysign(floor(fabs(x) + 0.5), x); }
+GTMI_DEV float round_away(float x) { return copysignf(floorf(fabsf(x) + 0.5f), x); }
+
+}  // namespace gtmi

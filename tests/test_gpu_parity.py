@@ -1,0 +1,153 @@
+"""gt:mi355x parity on the GPU: every golden case, plus full-size hot-path configs vs the C oracle.
+
+Small cases compare against the reference numpy-backend golden vectors (bit-exact unless the
+case states a tolerance: transcendental functions differ by ULPs between glibc and ocml).
+Full-size cases (BASELINE.json configs C2-C4) compare against the C oracle bit-exactly.
+"""
+
+import numpy as np
+import pytest
+
+import golden_utils as gu
+import stencil_cases as sc
+
+pytestmark = pytest.mark.gpu
+
+BACKEND = "gt:mi355x"
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch
+
+
+def _origin_of(case, name, ndim):
+    o = case.origin
+    if o is None:
+        return (0,) * ndim
+    if isinstance(o, dict):
+        return tuple(o.get(name, o.get("_all_", (0,) * ndim)))[:ndim]
+    return tuple(o)[:ndim]
+
+
+def run_case_on_gpu(case):
+    from gt4py_amd import gtscript, storage
+
+    stencil = gtscript.stencil(backend=BACKEND, definition=case.definition, externals=case.externals,
+                               name=f"gpu.{case.name}")
+    host = case.make_inputs()
+    dev = {}
+    for k, v in host.items():
+        if v is None:
+            dev[k] = None
+        else:
+            dev[k] = storage.from_array(v, backend=BACKEND, aligned_index=_origin_of(case, k, v.ndim))
+    kw = {}
+    if case.origin is not None:
+        kw["origin"] = case.origin
+    if case.domain is not None:
+        kw["domain"] = case.domain
+    stencil(**dev, **case.params, **kw)
+    return {k: (None if v is None else storage.to_numpy(v)) for k, v in dev.items()}
+
+
+@pytest.mark.parametrize("name", gu.available())
+def test_golden_case(name):
+    _torch()
+    case = sc.CASES[name]
+    _, outputs, _ = gu.load(name)
+    res = run_case_on_gpu(case)
+    for k, v in outputs.items():
+        gu.assert_match(res[k], v, rtol=case.rtol, atol=case.atol, name=f"{name}:{k}")
+
+
+# ---------------------------------------------------------------------------------------
+# full-size hot-path configurations (BASELINE.json configs) against the C oracle
+# ---------------------------------------------------------------------------------------
+
+
+def _alloc_fill(shape, dtype, rng, lo, hi, origin):
+    from gt4py_amd import storage
+
+    host = rng.uniform(lo, hi, size=shape).astype(dtype)
+    return host, storage.from_array(host, backend=BACKEND, aligned_index=origin)
+
+
+@pytest.mark.parametrize("dtype,ni,nj,nk", [(np.float64, 2048, 2048, 160), (np.float32, 1024, 1024, 64)])
+def test_hdiff_full_size_vs_c_oracle(dtype, ni, nj, nk):
+    _torch()
+    from gt4py_amd import gtscript, storage
+    from oracle import c_oracle
+
+    fn = sc.hdiff_f64 if dtype == np.float64 else sc.hdiff_f32
+    stencil = gtscript.stencil(backend=BACKEND, definition=fn, name=f"full.hdiff_{np.dtype(dtype).name}")
+    rng = np.random.default_rng(1337)
+    h = 2
+    in_h, in_d = _alloc_fill((ni + 2 * h, nj + 2 * h, nk), dtype, rng, -10, 10, (h, h, 0))
+    co_h, co_d = _alloc_fill((ni, nj, nk), dtype, rng, 0, 0.5, (0, 0, 0))
+    out_d = storage.zeros((ni, nj, nk), dtype, backend=BACKEND)
+    stencil(in_d, out_d, co_d, origin={"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)},
+            domain=(ni, nj, nk))
+    got = storage.to_numpy(out_d)
+    ref = np.zeros((ni, nj, nk), dtype=dtype, order="F")
+    org = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    c_oracle.horizontal_diffusion(np.asfortranarray(in_h), ref, np.asfortranarray(co_h), org, (ni, nj, nk))
+    gu.assert_match(got, ref, name="hdiff_full")
+
+
+def test_lap5_full_size_vs_c_oracle():
+    _torch()
+    from gt4py_amd import gtscript, storage
+    from oracle import c_oracle
+
+    ni, nj, nk = 1024, 1024, 80
+    stencil = gtscript.stencil(backend=BACKEND, definition=sc.lap5, name="full.lap5")
+    rng = np.random.default_rng(1337)
+    in_h, in_d = _alloc_fill((ni + 2, nj + 2, nk), np.float64, rng, -10, 10, (1, 1, 0))
+    out_d = storage.zeros((ni, nj, nk), np.float64, backend=BACKEND)
+    stencil(in_d, out_d, origin={"in_field": (1, 1, 0), "out_field": (0, 0, 0)}, domain=(ni, nj, nk))
+    ref = np.zeros((ni, nj, nk), order="F")
+    c_oracle.lap5(np.asfortranarray(in_h), ref, {"in_field": (1, 1, 0), "out_field": (0, 0, 0)}, (ni, nj, nk))
+    gu.assert_match(storage.to_numpy(out_d), ref, name="lap5_full")
+
+
+def test_tridiag_full_size_vs_c_oracle():
+    _torch()
+    from gt4py_amd import gtscript, storage
+    from oracle import c_oracle
+
+    ni, nj, nk = 1024, 1024, 160
+    stencil = gtscript.stencil(backend=BACKEND, definition=sc.tridiagonal_solver, name="full.tridiag")
+    rng = np.random.default_rng(1337)
+    hosts, devs = {}, {}
+    for name, lo, hi in (("inf", -1, 1), ("diag", 4, 5), ("sup", -1, 1), ("rhs", -10, 10)):
+        hosts[name], devs[name] = _alloc_fill((ni, nj, nk), np.float64, rng, lo, hi, (0, 0, 0))
+    hosts["out"] = np.zeros((ni, nj, nk))
+    devs["out"] = storage.zeros((ni, nj, nk), np.float64, backend=BACKEND)
+    stencil(**devs)
+    ref = {k: np.asfortranarray(v) for k, v in hosts.items()}
+    org = {k: (0, 0, 0) for k in ref}
+    c_oracle.tridiagonal_solver(ref["inf"], ref["diag"], ref["sup"], ref["rhs"], ref["out"], org, (ni, nj, nk))
+    for k in ("sup", "rhs", "out"):
+        gu.assert_match(storage.to_numpy(devs[k]), ref[k], name=f"tridiag_full:{k}")
+
+
+def test_outside_domain_untouched():
+    """Outputs are written inside the compute domain only (stencil_object.py contract)."""
+    torch = _torch()
+    from gt4py_amd import gtscript, storage
+
+    stencil = gtscript.stencil(backend=BACKEND, definition=sc.copy_stencil, name="gpu.copy_untouched")
+    a = storage.from_array(np.arange(10 * 9 * 7, dtype=np.float64).reshape(10, 9, 7), backend=BACKEND)
+    b = storage.full((10, 9, 7), -1.0, backend=BACKEND)
+    stencil(a, b, origin=(2, 3, 1), domain=(5, 4, 3))
+    bh = storage.to_numpy(b)
+    ah = storage.to_numpy(a)
+    mask = np.zeros_like(bh, dtype=bool)
+    mask[2:7, 3:7, 1:4] = True
+    assert (bh[mask] == ah[mask]).all()
+    assert (bh[~mask] == -1.0).all()
+    del torch
