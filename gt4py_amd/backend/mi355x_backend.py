@@ -169,6 +169,12 @@ class Mi355xBackend(BaseBackend):
     options = {
         "device_sync": {"versioning": False, "type": bool, "description": "synchronize the stream after each call"},
         "jchunk": {"versioning": True, "type": int, "description": "J rows per wavefront in plane kernels"},
+        "vector": {"versioning": True, "type": int, "description": "I elements per lane in plane kernels (1, 2, 4)"},
+        "prefetch": {"versioning": True, "type": int, "description": "rows loaded ahead in plane kernels"},
+        "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
+        "col_occupancy": {"versioning": True, "type": int, "description": "max column-kernel blocks per CU (0 = hw)"},
+        "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
+        "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

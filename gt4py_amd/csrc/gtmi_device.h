@@ -113,3 +113,33 @@ GTMI_DEV double round_away(double x) { return copysign(floor(fabs(x) + 0.5), x);
 GTMI_DEV float round_away(float x) { return copysignf(floorf(fabsf(x) + 0.5f), x); }
 
 }  // namespace gtmi
+
+namespace gtmi {
+// V contiguous elements of T, aligned to their size: one global_load/store of V*sizeof(T) bytes.
+template <typename T, int V> struct alignas(sizeof(T) * V) vec {
+    T v[V];
+};
+}  // namespace gtmi
+
+// Runtime switch GTMI_VECTOR=1 forces the scalar (V=1) plane kernels (host side, read once).
+#include <stdlib.h>
+static inline int gtmi_env_vector(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char* s = getenv("GTMI_VECTOR");
+        v = s ? atoi(s) : 0;
+    }
+    return v;
+}
+
+// Multiplier a with gcd(a, n) == 1 near n / golden ratio: w -> (w * a) mod n scatters work
+// items bijectively (host side).
+static inline int gtmi_coprime_multiplier(long long n) {
+    if (n <= 2) return 1;
+    long long a = (long long)(n * 0.6180339887) | 1;
+    for (;; a += 2) {
+        long long x = a, y = n;
+        while (y) { long long t = x % y; x = y; y = t; }
+        if (x == 1) return (int)(a % n);
+    }
+}

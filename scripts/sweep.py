@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of gt:mi355x codegen variants in ONE process (cdna guide §5.4 rule 24).
+
+    python scripts/sweep.py --config hdiff --variants "vector=1,prefetch=1;vector=2,prefetch=2"
+    python scripts/sweep.py --config hdiff --variants "..." --build-only   # prebuild on CPU
+
+Every variant's output is checked bit-for-bit against the first variant's output.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def parse_variants(text):
+    out = []
+    for part in text.split(";"):
+        part = part.strip()
+        if not part:
+            continue
+        d = {}
+        for kv in part.split(","):
+            k, v = kv.split("=")
+            d[k.strip()] = int(v) if v.strip().lstrip("-").isdigit() else v.strip()
+        out.append(d)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="hdiff")
+    ap.add_argument("--variants", required=True)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--build-only", action="store_true")
+    args = ap.parse_args()
+    import bench
+    from gt4py_amd import gtscript
+
+    sname, dtype, (ni, nj, nk), h, bpc = bench.CONFIGS[args.config]
+    defn = bench.stencil_defs()[(sname, dtype)]
+    variants = parse_variants(args.variants)
+    stencils = []
+    for i, v in enumerate(variants):
+        stencils.append(
+            gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"sweep.{args.config}.{i}", device_sync=False, **v)
+        )
+    if args.build_only:
+        print(f"built {len(stencils)} variants")
+        return
+    import torch
+
+    from gt4py_amd import storage
+
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    tdt = storage.torch_dtype(dtype)
+
+    def uniform(shape, lo, hi, aligned):
+        t = storage.empty(shape, dtype, backend="gt:mi355x", aligned_index=aligned)
+        t.copy_(torch.rand(shape, generator=gen, device=dev, dtype=tdt) * (hi - lo) + lo)
+        return t
+
+    if sname in ("horizontal_diffusion", "lap5"):
+        fin = uniform((ni + 2 * h, nj + 2 * h, nk), -10, 10, (h, h, 0))
+        outs = [storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x") for _ in variants]
+        if sname == "horizontal_diffusion":
+            coeff = uniform((ni, nj, nk), 0, 0.5, (0, 0, 0))
+            argsets = [(fin, o, coeff) for o in outs]
+            origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+        else:
+            argsets = [(fin, o) for o in outs]
+            origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
+        check = [o for o in outs]
+    elif sname == "tridiagonal_solver":
+        base = [uniform((ni, nj, nk), lo, hi, (0, 0, 0)) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0))]
+        argsets = []
+        check = []
+        for _ in variants:
+            fs = [base[0], base[1], base[2].clone(), base[3].clone(), storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x")]
+            argsets.append(tuple(fs))
+            check.append(fs[4])
+        origin = (0, 0, 0)
+    else:
+        a = uniform((ni, nj, nk), -10, 10, (0, 0, 0))
+        outs = [storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x") for _ in variants]
+        argsets = [(a, o) for o in outs]
+        check = outs
+        origin = (0, 0, 0)
+    dom = (ni, nj, nk)
+    for st, a in zip(stencils, argsets):
+        st(*a, origin=origin, domain=dom)
+    torch.cuda.synchronize()
+    if sname != "tridiagonal_solver":
+        ref = check[0]
+        for i, c in enumerate(check[1:], 1):
+            if not torch.equal(c, ref):
+                print(f"variant {i} {variants[i]} MISMATCH: {int((c != ref).sum())} cells")
+    times = [[] for _ in variants]
+    for r in range(args.rounds):
+        for i, (st, a) in enumerate(zip(stencils, argsets)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                st(*a, origin=origin, domain=dom, validate_args=False)
+            e1.record()
+            torch.cuda.synchronize()
+            times[i].append(e0.elapsed_time(e1) / args.reps)
+    res = []
+    for v, t in zip(variants, times):
+        med = float(np.median(t))
+        gbs = ni * nj * nk * bpc / (med * 1e-3) / 1e9
+        res.append({"variant": v, "median_ms": round(med, 4), "min_ms": round(min(t), 4), "GBps": round(gbs, 1),
+                    "frac": round(gbs / 8000, 4)})
+        print(json.dumps(res[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()

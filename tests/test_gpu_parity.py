@@ -151,3 +151,29 @@ def test_outside_domain_untouched():
     assert (bh[mask] == ah[mask]).all()
     assert (bh[~mask] == -1.0).all()
     del torch
+
+
+@pytest.mark.parametrize("name", ["hdiff_f64", "hdiff_f32", "suite_hdiff_weight", "multi_stage_temps", "lap5"])
+def test_scalar_fallback_layouts(name):
+    """K-contiguous (C-order) device tensors have sI != 1: the V=1 plane kernel must run and agree."""
+    torch = _torch()
+    from gt4py_amd import gtscript, storage
+
+    case = sc.CASES[name]
+    _, outputs, _ = gu.load(name)
+    stencil = gtscript.stencil(backend=BACKEND, definition=case.definition, externals=case.externals,
+                               name=f"gpu.{case.name}")
+    host = case.make_inputs()
+    dev = {k: (None if v is None else torch.from_numpy(np.ascontiguousarray(v)).cuda()) for k, v in host.items()}
+    kw = {}
+    if case.origin is not None:
+        kw["origin"] = case.origin
+    if case.domain is not None:
+        kw["domain"] = case.domain
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        stencil(**dev, **case.params, **kw)
+    for k, v in outputs.items():
+        gu.assert_match(storage.to_numpy(dev[k]), v, rtol=case.rtol, atol=case.atol, name=f"{name}:{k}")
