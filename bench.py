@@ -158,17 +158,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local_rank % ndev)
+    dev = torch.device("cuda", local_rank % ndev)
     dist = None
     if world > 1:
         from gt4py_amd.distributed import init_process_group
 
-        init_process_group("nccl")
+        # nccl (= RCCL over xGMI) on a real node; GTMI_DIST_BACKEND=gloo rehearses N ranks on one GPU
+        init_process_group(os.environ.get("GTMI_DIST_BACKEND", "nccl"))
         import torch.distributed as dist
 
     from gt4py_amd import gtscript, storage
-    from gt4py_amd.distributed import JHaloExchange
+    from gt4py_amd.distributed import HaloStencil
 
     sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[args.config]
     defs = stencil_defs()
@@ -194,33 +196,34 @@ def main():
         if sname == "horizontal_diffusion":
             coeff = uniform((ni, nj, nk), 0.0, 0.5, (0, 0, 0))
             call_args = (fin, out, coeff)
+            named = {"in_field": fin, "out_field": out, "coeff": coeff}
             origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
         else:
             call_args = (fin, out)
+            named = {"in_field": fin, "out_field": out}
             origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
         if world > 1:
-            halo = JHaloExchange(nj, h, rank, world)
-        halo_fields = [fin]
+            # J-strip of the global domain: exchange the in_field halo with the neighbours over
+            # RCCL while the interior rows compute, then the two boundary strips
+            halo = HaloStencil(stencil, ["in_field"], nj, h, rank, world)
     elif sname == "tridiagonal_solver":
         fields = [uniform((ni, nj, nk), lo, hi, (0, 0, 0)) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0))]
         call_args = tuple(fields)
         origin = (0, 0, 0)
-        halo_fields = []
     else:
         a = uniform((ni, nj, nk), -10, 10, (0, 0, 0))
         b = storage.zeros((ni, nj, nk), dtype, backend=be)
         call_args = (a, b)
         origin = (0, 0, 0)
-        halo_fields = []
     domain = (ni, nj, nk)
-    frozen = None
 
     def step(ev_pair=None):
-        if halo is not None:
-            halo.exchange(halo_fields)
         if ev_pair is not None:
             ev_pair[0].record()
-        stencil(*call_args, origin=origin, domain=domain, validate_args=False)
+        if halo is not None:
+            halo(named, origin, domain)
+        else:
+            stencil(*call_args, origin=origin, domain=domain, validate_args=False)
         if ev_pair is not None:
             ev_pair[1].record()
 
@@ -243,7 +246,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     if dist is not None:
-        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
+        tdev = dev if str(dist.get_backend()).lower() == "nccl" else "cpu"
+        t = torch.tensor([elapsed, kernel_ms], device=tdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
     cells_per_step = ni * nj * nk

@@ -12,12 +12,16 @@ K plane, so packing is one strided copy per face; messages are a few MB (SURVEY.
 2 x (8192+4) x 160 x 4 B = 10.5 MB per face for C5), i.e. one point-to-point xGMI transfer
 per neighbour -- there are no reductions, so no ring collective is involved.
 Global boundaries are plain input cells (no periodicity, as in the reference).
+
+``HaloStencil`` overlaps the exchange with compute: the rows that do not read the halo run
+while RCCL moves the faces (RCCL's own stream waits on the packing copies; the compute stream
+waits on the transfers only before unpacking), then the two boundary strips run.
 """
 
 from __future__ import annotations
 
 import dataclasses
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 
 @dataclasses.dataclass(frozen=True)
@@ -38,8 +42,14 @@ class JStrips:
         return j1 - j0
 
 
+def _backend_name(group=None) -> str:
+    import torch.distributed as dist
+
+    return str(dist.get_backend(group)).lower()
+
+
 class JHaloExchange:
-    """Exchange the J halo of one or more fields stored as [I, J_local + 2h, K] tensors.
+    """Exchange the J halo of fields stored as ``[I, J_local + 2h, K]`` tensors.
 
     Local row ``h + r`` holds global row ``j0 + r``; rows ``[0, h)`` and ``[h + nj, 2h + nj)``
     are the halos filled from the previous / next rank. On the first/last rank the outer halo
@@ -54,7 +64,14 @@ class JHaloExchange:
         self.group = group
         self.prev = rank - 1 if rank > 0 else None
         self.next = rank + 1 if rank < world_size - 1 else None
-        self._bufs = {}
+        self._bufs: Dict[Tuple, Dict] = {}
+        self._pending: List = []
+        self._stage_host: Optional[bool] = None
+
+    def _global_rank(self, r):
+        import torch.distributed as dist
+
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
 
     def _buffers(self, t):
         key = (t.data_ptr(), tuple(t.shape), t.dtype)
@@ -62,14 +79,18 @@ class JHaloExchange:
             import torch
 
             ni, _, nk = t.shape
-            mk = lambda: torch.empty((ni, self.h, nk), dtype=t.dtype, device=t.device)  # noqa: E731
+            dev = "cpu" if self._stage_host else t.device
+            mk = lambda: torch.empty((ni, self.h, nk), dtype=t.dtype, device=dev)  # noqa: E731
             self._bufs[key] = {"send_lo": mk(), "send_hi": mk(), "recv_lo": mk(), "recv_hi": mk()}
         return self._bufs[key]
 
-    def start(self, fields: List) -> List:
+    def start(self, fields: Sequence) -> List:
         """Pack faces and post the sends/receives; returns the pending work handles."""
         import torch.distributed as dist
 
+        if self._stage_host is None:
+            # gloo moves host memory only: stage device faces through the host (tests / CPU runs)
+            self._stage_host = _backend_name(self.group) == "gloo"
         ops = []
         h, nj = self.h, self.nj
         self._pending = []
@@ -77,12 +98,12 @@ class JHaloExchange:
             b = self._buffers(t)
             if self.prev is not None:
                 b["send_lo"].copy_(t[:, h : 2 * h, :])
-                ops.append(dist.P2POp(dist.isend, b["send_lo"], self.prev, self.group))
-                ops.append(dist.P2POp(dist.irecv, b["recv_lo"], self.prev, self.group))
+                ops.append(dist.P2POp(dist.isend, b["send_lo"], self._global_rank(self.prev), self.group))
+                ops.append(dist.P2POp(dist.irecv, b["recv_lo"], self._global_rank(self.prev), self.group))
             if self.next is not None:
                 b["send_hi"].copy_(t[:, nj : nj + h, :])
-                ops.append(dist.P2POp(dist.isend, b["send_hi"], self.next, self.group))
-                ops.append(dist.P2POp(dist.irecv, b["recv_hi"], self.next, self.group))
+                ops.append(dist.P2POp(dist.isend, b["send_hi"], self._global_rank(self.next), self.group))
+                ops.append(dist.P2POp(dist.irecv, b["recv_hi"], self._global_rank(self.next), self.group))
             self._pending.append((t, b))
         if not ops:
             return []
@@ -100,8 +121,48 @@ class JHaloExchange:
                 t[:, nj + h : nj + 2 * h, :].copy_(b["recv_hi"])
         self._pending = []
 
-    def exchange(self, fields: List) -> None:
+    def exchange(self, fields: Sequence) -> None:
         self.finish(self.start(fields))
+
+
+class HaloStencil:
+    """Run a stencil on one J strip of a decomposed domain, overlapping the halo exchange.
+
+    ``halo_fields`` are the arguments read at J offsets; they carry ``halo`` extra rows on
+    each side. The call splits the local domain into the interior rows (no halo read,
+    computed while the faces are in flight) and the two boundary strips (computed after).
+    """
+
+    def __init__(self, stencil, halo_fields: Sequence[str], nj_local: int, halo: int, rank: int, world_size: int,
+                 group=None, overlap: bool = True):
+        self.stencil = stencil
+        self.halo_fields = list(halo_fields)
+        self.exchange = JHaloExchange(nj_local, halo, rank, world_size, group)
+        self.h = halo
+        self.nj = nj_local
+        self.overlap = overlap and world_size > 1 and nj_local > 2 * halo
+
+    def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
+        return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
+
+    def __call__(self, args: Dict, origin: Dict[str, Tuple[int, int, int]], domain: Tuple[int, int, int],
+                 **params) -> None:
+        ni, nj, nk = domain
+        assert nj == self.nj, (nj, self.nj)
+        fields = [args[n] for n in self.halo_fields]
+        kw = dict(args)
+        kw.update(params)
+        if not self.overlap:
+            self.exchange.exchange(fields)
+            self.stencil(**kw, origin=origin, domain=domain, validate_args=False)
+            return
+        h = self.h
+        works = self.exchange.start(fields)
+        # interior rows [h, nj - h): read rows [0, nj) of the halo'ed fields only
+        self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
+        self.exchange.finish(works)
+        self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
+        self.stencil(**kw, origin=self._shifted(origin, nj - h), domain=(ni, h, nk), validate_args=False)
 
 
 def init_process_group(backend: Optional[str] = None):
@@ -115,7 +176,7 @@ def init_process_group(backend: Optional[str] = None):
         return dist.get_rank(), dist.get_world_size()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("GTMI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         lr = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(lr)

@@ -1,0 +1,111 @@
+"""Multi-process J-strip decomposition + halo exchange (gloo on CPU, world sizes 2 and 3).
+
+Each rank owns a J strip whose interior halo rows start as NaN: only a correct exchange fills
+them. The distributed result (interior/boundary split with the exchange overlapped) must equal
+the single-domain result of the same stencil bit-for-bit (hdiff f64 and the lap5 stencil).
+"""
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, outdir, which):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import stencil_cases as sc
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed import HaloStencil, JStrips
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ni, njg, nk, h = 12, 23, 4, (2 if which == "hdiff" else 1)
+    rng = np.random.default_rng(11)
+    gin = rng.uniform(-10, 10, (ni + 2 * h, njg + 2 * h, nk))
+    gco = rng.uniform(0, 0.5, (ni, njg, nk))
+    j0, j1 = JStrips(njg, world).bounds(rank)
+    nj = j1 - j0
+    lin = gin[:, j0 : j1 + 2 * h, :].copy()
+    if rank > 0:
+        lin[:, :h, :] = np.nan
+    if rank < world - 1:
+        lin[:, nj + h :, :] = np.nan
+    t_in = torch.from_numpy(lin)
+    t_out = torch.zeros((ni, nj, nk), dtype=torch.float64)
+    if which == "hdiff":
+        st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist.hdiff")
+        args = {"in_field": t_in, "out_field": t_out, "coeff": torch.from_numpy(gco[:, j0:j1, :].copy())}
+        origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    else:
+        st = gtscript.stencil(backend="numpy", definition=sc.lap5, name="dist.lap5")
+        args = {"in_field": t_in, "out_field": t_out}
+        origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
+    runner = HaloStencil(st, ["in_field"], nj, h, rank, world)
+    runner(args, origin, (ni, nj, nk))
+    np.save(os.path.join(outdir, f"out_{rank}.npy"), t_out.numpy())
+    # the halos now hold the neighbours' rows
+    np.save(os.path.join(outdir, f"in_{rank}.npy"), t_in.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,which", [(2, "hdiff"), (3, "hdiff"), (2, "lap5")])
+def test_jstrip_halo_exchange_matches_single_domain(tmp_path, world, which):
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, REPO)
+    import stencil_cases as sc
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed import JStrips
+
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path), which), nprocs=world, join=True)
+    ni, njg, nk, h = 12, 23, 4, (2 if which == "hdiff" else 1)
+    rng = np.random.default_rng(11)
+    gin = rng.uniform(-10, 10, (ni + 2 * h, njg + 2 * h, nk))
+    gco = rng.uniform(0, 0.5, (ni, njg, nk))
+    ref = np.zeros((ni, njg, nk))
+    if which == "hdiff":
+        st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist.hdiff")
+        st(gin.copy(), ref, gco, origin={"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)})
+    else:
+        st = gtscript.stencil(backend="numpy", definition=sc.lap5, name="dist.lap5")
+        st(gin.copy(), ref, origin={"in_field": (h, h, 0), "out_field": (0, 0, 0)})
+    parts = [np.load(tmp_path / f"out_{r}.npy") for r in range(world)]
+    got = np.concatenate(parts, axis=1)
+    assert np.array_equal(got, ref)
+    strips = JStrips(njg, world)
+    for r in range(world):
+        j0, j1 = strips.bounds(r)
+        assert np.array_equal(np.load(tmp_path / f"in_{r}.npy"), gin[:, j0 : j1 + 2 * h, :])
+
+
+def test_jstrips_cover_domain():
+    from gt4py_amd.distributed import JStrips
+
+    for n in (1, 7, 64, 2048):
+        for w in (1, 2, 3, 8):
+            if w > n:
+                continue
+            s = JStrips(n, w)
+            b = [s.bounds(r) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+            assert max(s.size(r) for r in range(w)) - min(s.size(r) for r in range(w)) <= 1
