@@ -15,40 +15,20 @@ There is no CPU fallback: without the compiled library or a ROCm device the call
 
 from __future__ import annotations
 
-import ctypes
 import time
-from typing import Any, Dict, Tuple
-
-import numpy as np
 
 from gt4py_amd.backend.base import BaseBackend, register
 from gt4py_amd.codegen import hip as hipgen
 from gt4py_amd.codegen.plan import make_plan
-from gt4py_amd.runtime import ffi, jit
+from gt4py_amd.runtime import jit
+from gt4py_amd.runtime.launcher import StencilLauncher
 from gt4py_amd.storage.layout import layout_checker_factory, layout_maker_factory
 
 _layout = layout_maker_factory((2, 1, 0))
 
 
-def _tensor_of(obj):
-    import torch
-
-    if isinstance(obj, torch.Tensor):
-        t = obj
-    elif hasattr(obj, "__cuda_array_interface__"):
-        t = torch.as_tensor(obj, device="cuda")
-    else:
-        raise TypeError(
-            f"gt:mi355x expects device arrays (torch ROCm tensors or objects with __cuda_array_interface__), "
-            f"got {type(obj).__name__}; allocate with gt4py_amd.storage.*(backend='gt:mi355x')"
-        )
-    if not t.is_cuda:
-        raise TypeError("gt:mi355x expects tensors on the ROCm device (tensor.is_cuda is False)")
-    return t
-
-
 class _Compiled:
-    """Everything a call needs: the library and the argument layout."""
+    """The generated source, its library and the launcher that calls it."""
 
     def __init__(self, analysis, plan, source, signature, lib_path, options):
         self.analysis = analysis
@@ -57,110 +37,17 @@ class _Compiled:
         self.signature = signature
         self.lib_path = lib_path
         self.options = options
-        self._lib = None
-        st = analysis.stencil
-        self.field_params = st.field_params()
-        self.scalar_params = st.scalar_params()
-        self.n_fields = len(self.field_params) + len(plan.scratch)
-        self.scratch_decls = [(t, st.decl(t).dtype) for t in plan.scratch]
-        self._scratch_cache: Dict[Tuple, Any] = {}
-
-    @property
-    def lib(self):
-        if self._lib is None:
-            self._lib = ffi.load_library(self.lib_path)
-        return self._lib
-
-    def _scratch(self, domain, device):
-        key = (tuple(domain), str(device))
-        if key not in self._scratch_cache:
-            import torch
-
-            from gt4py_amd.storage import torch_dtype
-
-            ni, nj, nk = domain
-            out = []
-            for name, dtype in self.scratch_decls:
-                (ilo, ihi), (jlo, jhi) = self.plan.scratch_extent[name]
-                si = ni + ilo + ihi
-                sj = nj + jlo + jhi
-                pi = -(-si // 32) * 32
-                buf = torch.empty(pi * sj * nk, dtype=torch_dtype(dtype.np_dtype), device=device)
-                out.append((buf, (si, sj, nk), (1, pi, pi * sj), (ilo, jlo, 0)))
-            self._scratch_cache[key] = out
-        return self._scratch_cache[key]
+        self.launcher = StencilLauncher(lib_path, analysis.stencil.name)
 
     def __call__(self, domain, origin, exec_info, kwargs):
-        import torch
-
-        ni, nj, nk = (int(d) for d in domain)
-        fields = (ffi.GtmiField * self.n_fields)()
-        device = None
-        for idx, decl in enumerate(self.field_params):
-            arr = kwargs.get(decl.name)
-            f = fields[idx]
-            if arr is None:
-                f.data = None
-                continue
-            t = _tensor_of(arr)
-            device = t.device
-            want = decl.dtype.np_dtype
-            from gt4py_amd.storage import numpy_dtype_of
-
-            if numpy_dtype_of(t) != want:
-                raise TypeError(f"The dtype of field '{decl.name}' is '{numpy_dtype_of(t)}' instead of '{want}'")
-            if decl.data_dims:
-                raise NotImplementedError("data dimensions are not supported by gt:mi355x yet")
-            org = origin[decl.name]
-            mask = decl.mask
-            st = t.stride()
-            sh = t.shape
-            d = 0
-            for ax in range(3):
-                if mask[ax]:
-                    f.strides[ax] = st[d]
-                    f.shape[ax] = sh[d]
-                    f.origin[ax] = int(org[d])
-                    d += 1
-                else:
-                    f.strides[ax] = 0
-                    f.shape[ax] = 1
-                    f.origin[ax] = 0
-            f.data = t.data_ptr()
-            f.dtype = ffi.DTYPE_IDS[want.name]
-            f.ndim = sum(mask)
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device())
-        base = len(self.field_params)
-        for j, (buf, shape, strides, org) in enumerate(self._scratch((ni, nj, nk), device)):
-            f = fields[base + j]
-            f.data = buf.data_ptr()
-            for ax in range(3):
-                f.strides[ax] = strides[ax]
-                f.shape[ax] = shape[ax]
-                f.origin[ax] = org[ax]
-            f.ndim = 3
-            f.dtype = ffi.DTYPE_IDS[self.scratch_decls[j][1].np_dtype.name]
-        n_sc = len(self.scalar_params)
-        scalars = (ffi.GtmiScalar * max(1, n_sc))()
-        for j, s in enumerate(self.scalar_params):
-            v = kwargs.get(s.name)
-            if v is None:
-                v = 0
-            ffi.set_scalar(scalars[j], s.dtype.np_dtype.name, v)
-        dom = (ctypes.c_int64 * 3)(ni, nj, nk)
-        with torch.cuda.device(device):
-            stream = torch.cuda.current_stream(device)
-            if exec_info is not None:
-                torch.cuda.synchronize(device)
-                exec_info["run_cpp_start_time"] = time.perf_counter()
-            rc = self.lib.run(dom, fields, self.n_fields, scalars, n_sc, ctypes.c_void_p(stream.cuda_stream))
-            if rc != 0:
-                raise RuntimeError(f"gt:mi355x stencil '{self.analysis.stencil.name}' failed: {self.lib.last_error()}")
-            if self.options.get("device_sync", True) or exec_info is not None:
-                stream.synchronize()
-            if exec_info is not None:
-                exec_info["run_cpp_end_time"] = time.perf_counter()
+        self.launcher(
+            domain,
+            origin,
+            kwargs,
+            kwargs,
+            device_sync=bool(self.options.get("device_sync", True)),
+            exec_info=exec_info,
+        )
 
 
 @register

@@ -1170,17 +1170,19 @@ def generate(analysis: StencilAnalysis, plan: KernelPlan, opts: Dict) -> Tuple[s
 
     signature = {
         "abi": 1,
-        "name": st.name,
         "fields": [
             {"name": p.name, "dtype": p.dtype.name.lower(), "axes": list(p.axes)} for p in st.field_params()
         ],
-        "scratch": [{"name": t, "dtype": st.decl(t).dtype.name.lower()} for t in plan.scratch],
+        "scratch": [
+            {"name": t, "dtype": st.decl(t).dtype.name.lower(), "extent": [list(e) for e in plan.scratch_extent[t]]}
+            for t in plan.scratch
+        ],
         "scalars": [{"name": s.name, "dtype": s.dtype.name.lower()} for s in st.scalar_params()],
         "kernels": [type(k).__name__ for k in plan.kernels],
     }
     sig_json = json.dumps(signature).replace("\\", "\\\\").replace('"', '\\"')
     n_scalars = len(st.scalar_params())
-    src = f"""// Generated by gt4py_amd (gt:mi355x) for stencil '{st.name}'. Do not edit.
+    src = f"""// Generated by gt4py_amd (gt:mi355x). Do not edit.
 #include "gtmi_device.h"
 #include "gtmi.h"
 #include <string.h>

@@ -48,8 +48,9 @@ def hipcc_path() -> str:
 
 
 def cache_root() -> str:
-    root = os.environ.get("GT_CACHE_ROOT", REPO_ROOT)
-    name = os.environ.get("GT_CACHE_DIR_NAME", ".gt_cache")
+    # in-tree by default so that libraries built in the build container travel with the repo
+    root = os.environ.get("GTMI_CACHE_ROOT", REPO_ROOT)
+    name = os.environ.get("GTMI_CACHE_DIR_NAME", ".gt_cache")
     return os.path.join(root, name, "gt_mi355x")
 
 

@@ -1,0 +1,156 @@
+"""Host-side launcher of a generated stencil library, driven by its self-description.
+
+Every library exports ``gtmi_stencil_signature()`` (JSON: API fields with dtype/axes, scratch
+temporaries with dtype/extent, scalars with dtype). ``StencilLauncher`` needs nothing else:
+it is shared by the native ``gt:mi355x`` StencilObject and by the adapter that registers the
+backend inside the reference gt4py (``gt4py_amd.gt4py_plugin``).
+
+Per call: pack one ``gtmi_field`` per API field (borrowed device pointer, element strides,
+origin, shape), append the cached scratch buffers, pack the scalars, call
+``gtmi_stencil_run`` on torch's current HIP stream, optionally synchronize.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import time
+from typing import Any, Dict, Tuple
+
+import numpy as np
+
+from gt4py_amd.runtime import ffi
+
+_AXES = ("I", "J", "K")
+
+
+def device_tensor(obj):
+    """The torch view of a device array argument (torch tensor or __cuda_array_interface__)."""
+    import torch
+
+    if isinstance(obj, torch.Tensor):
+        t = obj
+    elif hasattr(obj, "__cuda_array_interface__"):
+        t = torch.as_tensor(obj, device="cuda")
+    else:
+        raise TypeError(
+            f"gt:mi355x expects device arrays (torch ROCm tensors or objects with __cuda_array_interface__), "
+            f"got {type(obj).__name__}; allocate with gt4py_amd.storage.*(backend='gt:mi355x')"
+        )
+    if not t.is_cuda:
+        raise TypeError("gt:mi355x expects tensors on the ROCm device (tensor.is_cuda is False)")
+    return t
+
+
+def _np_dtype_of(t) -> np.dtype:
+    from gt4py_amd.storage import numpy_dtype_of
+
+    return numpy_dtype_of(t)
+
+
+class StencilLauncher:
+    def __init__(self, lib_path: str, name: str = ""):
+        self.lib_path = lib_path
+        self.name = name
+        self._lib = None
+        self._scratch_cache: Dict[Tuple, Any] = {}
+
+    @property
+    def lib(self) -> ffi.StencilLibrary:
+        if self._lib is None:
+            self._lib = ffi.load_library(self.lib_path)
+            sig = self._lib.signature
+            self.fields = sig["fields"]
+            self.scratch = sig["scratch"]
+            self.scalars = sig["scalars"]
+            self.n_fields = len(self.fields) + len(self.scratch)
+        return self._lib
+
+    def _scratch_buffers(self, domain, device):
+        key = (tuple(domain), str(device))
+        if key not in self._scratch_cache:
+            import torch
+
+            from gt4py_amd.storage import torch_dtype
+
+            ni, nj, nk = domain
+            out = []
+            for s in self.scratch:
+                (ilo, ihi), (jlo, jhi) = s["extent"]
+                si, sj = ni + ilo + ihi, nj + jlo + jhi
+                pi = -(-si // 32) * 32
+                buf = torch.empty(pi * sj * nk, dtype=torch_dtype(np.dtype(s["dtype"])), device=device)
+                out.append((buf, (si, sj, nk), (1, pi, pi * sj), (ilo, jlo, 0), s["dtype"]))
+            self._scratch_cache[key] = out
+        return self._scratch_cache[key]
+
+    def __call__(self, domain, origin, arrays: Dict[str, Any], params: Dict[str, Any], *, device_sync=True,
+                 exec_info=None) -> None:
+        import torch
+
+        lib = self.lib
+        ni, nj, nk = (int(d) for d in domain)
+        fields = (ffi.GtmiField * self.n_fields)()
+        device = None
+        for idx, decl in enumerate(self.fields):
+            name = decl["name"]
+            arr = arrays.get(name)
+            f = fields[idx]
+            if arr is None:
+                f.data = None
+                continue
+            t = device_tensor(arr)
+            device = t.device
+            want = np.dtype(decl["dtype"])
+            got = _np_dtype_of(t)
+            if got != want:
+                raise TypeError(f"The dtype of field '{name}' is '{got}' instead of '{want}'")
+            org = origin[name]
+            axes = decl["axes"]
+            st = t.stride()
+            sh = t.shape
+            if len(sh) != len(axes):
+                raise ValueError(f"Storage for '{name}' has {len(sh)} dimensions, expected {len(axes)} ({axes})")
+            d = 0
+            for ax in range(3):
+                if _AXES[ax] in axes:
+                    f.strides[ax] = st[d]
+                    f.shape[ax] = sh[d]
+                    f.origin[ax] = int(org[d])
+                    d += 1
+                else:
+                    f.strides[ax] = 0
+                    f.shape[ax] = 1
+                    f.origin[ax] = 0
+            f.data = t.data_ptr()
+            f.dtype = ffi.DTYPE_IDS[want.name]
+            f.ndim = len(axes)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        base = len(self.fields)
+        for j, (buf, shape, strides, org, dt) in enumerate(self._scratch_buffers((ni, nj, nk), device)):
+            f = fields[base + j]
+            f.data = buf.data_ptr()
+            for ax in range(3):
+                f.strides[ax] = strides[ax]
+                f.shape[ax] = shape[ax]
+                f.origin[ax] = org[ax]
+            f.ndim = 3
+            f.dtype = ffi.DTYPE_IDS[np.dtype(dt).name]
+        n_sc = len(self.scalars)
+        scalars = (ffi.GtmiScalar * max(1, n_sc))()
+        for j, s in enumerate(self.scalars):
+            v = params.get(s["name"])
+            ffi.set_scalar(scalars[j], s["dtype"], 0 if v is None else v)
+        dom = (ctypes.c_int64 * 3)(ni, nj, nk)
+        with torch.cuda.device(device):
+            stream = torch.cuda.current_stream(device)
+            if exec_info is not None:
+                stream.synchronize()
+                exec_info["run_cpp_start_time"] = time.perf_counter()
+            rc = lib.run(dom, fields, self.n_fields, scalars, n_sc, ctypes.c_void_p(stream.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"gt:mi355x stencil '{self.name}' failed: {lib.last_error()}")
+            if device_sync or exec_info is not None:
+                stream.synchronize()
+            if exec_info is not None:
+                exec_info["run_cpp_end_time"] = time.perf_counter()

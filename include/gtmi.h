@@ -71,7 +71,7 @@ typedef union gtmi_scalar {
 int gtmi_stencil_run(const int64_t* domain, const gtmi_field* fields, int32_t n_fields,
                      const gtmi_scalar* scalars, int32_t n_scalars, void* stream);
 
-/* JSON description: {"abi":1,"name":...,"fields":[...],"scratch":[...],"scalars":[...],"kernels":[...]} */
+/* JSON description: {"abi":1,"fields":[...],"scratch":[...],"scalars":[...],"kernels":[...]} */
 const char* gtmi_stencil_signature(void);
 
 /* Message of the last failing gtmi_stencil_run on this thread ("" if none). */
