@@ -61,7 +61,9 @@ class Mi355xBackend(BaseBackend):
         "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
         "col_occupancy": {"versioning": True, "type": int, "description": "max column-kernel blocks per CU (0 = hw)"},
         "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
-        "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural)"},
+        "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow)"},
+        "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},
+        "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

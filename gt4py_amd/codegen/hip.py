@@ -465,6 +465,12 @@ class PlaneGen:
             t_start = min(t_start, -(v.needed_lo + v.lead))
         self.t_start = t_start
 
+    def _nt_load(self, v: Val) -> bool:
+        """Non-temporal loads for streams read once (no IJ offsets), if enabled."""
+        if not self.opts.get("nt_load", 1):
+            return False
+        return v.needed_ilo == 0 and v.needed_ihi == 0 and v.depth == 1
+
     def _lane_range(self, v: Val) -> Tuple[int, int]:
         """Lanes whose elements hold positions the value is needed at (inclusive)."""
         lo_pos = self.h_lo - v.needed_ilo
@@ -537,7 +543,12 @@ class PlaneGen:
                 B.append("const int w = (int)(((long long)w0x * p.perm_a) % nb);  // bijective scatter")
             else:
                 B.append("const int w = w0x;")
-        if order == 1:
+        if order == 4:  # chunks slowest: chunk c+1 starts as chunk c ends on the same XCD (halo rows warm)
+            B.append("const int sg = w % p.n_sgroups;")
+            B.append("const int rest = w / p.n_sgroups;")
+            B.append("const int kk = p.k0 + rest % p.nks;")
+            B.append("const int chunk = rest / p.nks;")
+        elif order == 1:
             B.append("const int kk = p.k0 + w % p.nks;")
             B.append("const int rest = w / p.nks;")
             B.append("const int sg = rest % p.n_sgroups;")
@@ -591,16 +602,24 @@ class PlaneGen:
                 f"    if (ln_{v.c}) {{",
             ]
             if V == 1:
-                out.append(f"        {dests[0]} = p.p_{c}[li_{c} + ro];")
+                nt = "true" if self._nt_load(v) else "false"
+                out.append(f"        {dests[0]} = gtmi::sload<{v.dtype.ctype}, {nt}>(p.p_{c} + li_{c} + ro);")
             else:
                 t = v.dtype.ctype
+                nt = "true" if self._nt_load(v) else "false"
                 out.append(f"        if (vok_{c}) {{")
-                out.append(
-                    f"            const gtmi::vec<{t}, {V}> tmp = "
-                    f"*reinterpret_cast<const gtmi::vec<{t}, {V}>*>(p.p_{c} + pos + ro);"
-                )
-                for e in range(V):
-                    out.append(f"            {dests[e]} = tmp.v[{e}];")
+                if v.dtype.itemsize >= 4:
+                    out.append(f"            {t} tmp[{V}];")
+                    out.append(f"            gtmi::vload<{t}, {V}, {nt}>(p.p_{c} + pos + ro, tmp);")
+                    for e in range(V):
+                        out.append(f"            {dests[e]} = tmp[{e}];")
+                else:
+                    out.append(
+                        f"            const gtmi::vec<{t}, {V}> tmp = "
+                        f"*reinterpret_cast<const gtmi::vec<{t}, {V}>*>(p.p_{c} + pos + ro);"
+                    )
+                    for e in range(V):
+                        out.append(f"            {dests[e]} = tmp.v[{e}];")
                 out.append("        } else {")
                 for e in range(V):
                     out.append(
@@ -678,16 +697,24 @@ class PlaneGen:
                 econd = [f"own_{e}" for e in range(V)]
             S.append(f"if ({rcond}) {{")
             S.append(f"    const int64_t ro = (int64_t)({row}) * p.sJ_{c} + (int64_t)kk * p.sK_{c};")
+            nts = "true" if (self.opts.get("nt_store", 1) and name not in self.scratch) else "false"
             if V == 1:
-                S.append(f"    if ({econd[0]}) p.p_{c}[(int64_t)i_0 * p.sI_{c} + ro] = {v.c}_0_0;")
+                S.append(
+                    f"    if ({econd[0]}) gtmi::sstore<{v.dtype.ctype}, {nts}>(p.p_{c} + (int64_t)i_0 * p.sI_{c} + ro, "
+                    f"{v.c}_0_0);"
+                )
             else:
                 t = v.dtype.ctype
                 allc = " && ".join(f"({x})" for x in econd)
                 S.append(f"    if (vok_{c} && {allc}) {{")
-                S.append(f"        gtmi::vec<{t}, {V}> tmp;")
-                for e in range(V):
-                    S.append(f"        tmp.v[{e}] = {v.c}_0_{e};")
-                S.append(f"        *reinterpret_cast<gtmi::vec<{t}, {V}>*>(p.p_{c} + pos + ro) = tmp;")
+                if v.dtype.itemsize >= 4:
+                    S.append(f"        const {t} tmp[{V}] = {{{', '.join(f'{v.c}_0_{e}' for e in range(V))}}};")
+                    S.append(f"        gtmi::vstore<{t}, {V}, {nts}>(p.p_{c} + pos + ro, tmp);")
+                else:
+                    S.append(f"        gtmi::vec<{t}, {V}> tmp;")
+                    for e in range(V):
+                        S.append(f"        tmp.v[{e}] = {v.c}_0_{e};")
+                    S.append(f"        *reinterpret_cast<gtmi::vec<{t}, {V}>*>(p.p_{c} + pos + ro) = tmp;")
                 S.append("    } else {")
                 for e in range(V):
                     S.append(f"        if ({econd[e]}) p.p_{c}[(int64_t)i_{e} * p.sI_{c} + ro] = {v.c}_0_{e};")
@@ -913,6 +940,28 @@ class ColumnGen:
                             used.append(self.slots[acc.name])
                         if w:
                             written.add(acc.name)
+        # cache policy: non-temporal loads of read-once streams (never written here, one IJ offset)
+        # and non-temporal stores of fields no other loop of this kernel reads back
+        keys: Dict[str, Set[Tuple[int, int]]] = {}
+        read_loops: Dict[str, Set[int]] = {}
+        write_loops: Dict[str, Set[int]] = {}
+        for li in self.kernel.loops:
+            for sec in st.vertical_loops[li].sections:
+                for acc, w in iter_accesses(sec.body):
+                    if not isinstance(acc, ir.FieldAccess):
+                        continue
+                    (write_loops if w else read_loops).setdefault(acc.name, set()).add(li)
+                    if not w:
+                        keys.setdefault(acc.name, set()).add(acc.offset[:2])
+        self.nt_loads = set()
+        self.nt_stores = set()
+        if self.opts.get("nt_load", 1):
+            self.nt_loads = {n for n, ks in keys.items() if n not in write_loops and len(ks) == 1 and self._mem(n)}
+        if self.opts.get("nt_store", 1):
+            self.nt_stores = {
+                n for n, wl in write_loops.items()
+                if self._mem(n) and n not in self.scratch and not (read_loops.get(n, set()) - wl)
+            }
         scalars = st.scalar_params()
         L = [f"struct K{k}Params {{"]
         for s in used:
@@ -990,13 +1039,22 @@ class ColumnGen:
             rng = win[(name, di, dj)]
             return f"w{li}_{cname(name)}_{_sgn(di)}_{_sgn(dj)}_{d - rng[0]}"
 
-        def mem_index(name, di, dj, kexpr):
+        def mem_ptr(name, di, dj, kexpr):
             c = cname(name)
             return (
-                f"p.p_{c}[(int64_t)gtmi::clampi(i + ({di}), p.ilo_{c}, p.ihi_{c}) * p.sI_{c} + "
+                f"p.p_{c} + ((int64_t)gtmi::clampi(i + ({di}), p.ilo_{c}, p.ihi_{c}) * p.sI_{c} + "
                 f"(int64_t)gtmi::clampi(j + ({dj}), p.jlo_{c}, p.jhi_{c}) * p.sJ_{c} + "
-                f"(int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c}]"
+                f"(int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
             )
+
+        def mem_index(name, di, dj, kexpr):
+            """A load expression (non-temporal for read-once streams)."""
+            nt = "true" if name in self.nt_loads else "false"
+            return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
+
+        def mem_store(name, kexpr, value):
+            nt = "true" if name in self.nt_stores else "false"
+            return f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
 
         P = int(self.opts.get("kprefetch", 0))
         step = "+" if fwd else "-"
@@ -1096,20 +1154,21 @@ class ColumnGen:
 
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
             for s in sec.body:
-                body += self._stmt(s, rend, wvar, mem_index)
+                body += self._stmt(s, rend, wvar, mem_store)
             out += ["            " + x for x in body]
             out.append("        }")
             out.append("    }")
         out.append("}")
         return out
 
-    def _stmt(self, s, rend, wvar, mem_index) -> List[str]:
+    def _stmt(self, s, rend, wvar, mem_store) -> List[str]:
+        mem_index = mem_store
         if isinstance(s, ir.Assign):
             name = s.target.name
             tgt = wvar(name, 0, 0, 0)
             out = [f"{tgt} = {rend(s.value)};"]
             if self._mem(name):
-                out.append(f"{mem_index(name, 0, 0, 'k')} = {tgt};")
+                out.append(mem_store(name, "k", tgt))
             return out
         if isinstance(s, ir.If):
             out = [f"if ({rend(s.cond)}) {{"]

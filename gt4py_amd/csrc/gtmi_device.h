@@ -143,3 +143,29 @@ static inline int gtmi_coprime_multiplier(long long n) {
         if (x == 1) return (int)(a % n);
     }
 }
+
+namespace gtmi {
+// 16-B-per-lane memory ops on clang ext vectors (bool/int8/int16 use the struct path).
+template <typename T, int V> using evec = T __attribute__((ext_vector_type(V)));
+
+template <typename T, int V, bool NT> GTMI_DEV void vload(const T* p, T (&out)[V]) {
+    const evec<T, V>* q = reinterpret_cast<const evec<T, V>*>(p);
+    evec<T, V> x;
+    if constexpr (NT) x = __builtin_nontemporal_load(q); else x = *q;
+#pragma unroll
+    for (int e = 0; e < V; ++e) out[e] = x[e];
+}
+template <typename T, int V, bool NT> GTMI_DEV void vstore(T* p, const T (&in)[V]) {
+    evec<T, V> x;
+#pragma unroll
+    for (int e = 0; e < V; ++e) x[e] = in[e];
+    evec<T, V>* q = reinterpret_cast<evec<T, V>*>(p);
+    if constexpr (NT) __builtin_nontemporal_store(x, q); else *q = x;
+}
+template <typename T, bool NT> GTMI_DEV T sload(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p); else return *p;
+}
+template <typename T, bool NT> GTMI_DEV void sstore(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
+}
+}  // namespace gtmi

@@ -52,7 +52,26 @@ def main(prof_dir, tag):
               f"rocprof {avg:.4f} ms  frac {e['roofline']['frac']:.3f}  "
               f"FETCH {e.get('FETCH_SIZE_KiB_per_dispatch', float('nan')) / 1024:.1f} MiB  "
               f"WRITE {e.get('WRITE_SIZE_KiB_per_dispatch', float('nan')) / 1024:.1f} MiB")
+        fetch, write = e.get("FETCH_SIZE_KiB_per_dispatch"), e.get("WRITE_SIZE_KiB_per_dispatch")
+        if fetch is not None and write is not None:
+            # bench.py reads roofline.traffic from here (per-launch HBM bytes, gfx950 correction)
+            with open(os.path.join("profiles", f"pmc_{cfg}.json"), "w") as f:
+                json.dump({
+                    "config": cfg,
+                    "workload": e["workload"],
+                    "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
+                    "fetch_size_kib": round(fetch, 1),
+                    "write_size_kib": round(write, 1),
+                    "correction": CORRECTION,
+                    "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
+                              f"bench.py --config {cfg} (profiles/{tag}_summary.json)",
+                }, f, indent=1)
     return path
+
+
+CORRECTION = ("hbm = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 B: on gfx950 FETCH_SIZE reports half the bytes of a "
+              "wide coalesced read (MI355X_MICROARCH.md HBM section); calibrated on the copy stencil "
+              "(1280 MiB read -> FETCH 640 MiB, WRITE 1280 MiB exact)")
 
 
 if __name__ == "__main__":

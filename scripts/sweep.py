@@ -71,7 +71,8 @@ def main():
 
     if sname in ("horizontal_diffusion", "lap5"):
         fin = uniform((ni + 2 * h, nj + 2 * h, nk), -10, 10, (h, h, 0))
-        outs = [storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x") for _ in variants]
+        shared = storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x")
+        outs = [shared for _ in variants]  # one buffer: HBM placement is identical for every variant
         if sname == "horizontal_diffusion":
             coeff = uniform((ni, nj, nk), 0, 0.5, (0, 0, 0))
             argsets = [(fin, o, coeff) for o in outs]
@@ -91,19 +92,21 @@ def main():
         origin = (0, 0, 0)
     else:
         a = uniform((ni, nj, nk), -10, 10, (0, 0, 0))
-        outs = [storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x") for _ in variants]
+        shared = storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x")
+        outs = [shared for _ in variants]
         argsets = [(a, o) for o in outs]
         check = outs
         origin = (0, 0, 0)
     dom = (ni, nj, nk)
-    for st, a in zip(stencils, argsets):
+    ref = None
+    for i, (st, a) in enumerate(zip(stencils, argsets)):
         st(*a, origin=origin, domain=dom)
-    torch.cuda.synchronize()
-    if sname != "tridiagonal_solver":
-        ref = check[0]
-        for i, c in enumerate(check[1:], 1):
-            if not torch.equal(c, ref):
-                print(f"variant {i} {variants[i]} MISMATCH: {int((c != ref).sum())} cells")
+        torch.cuda.synchronize()
+        if sname != "tridiagonal_solver":
+            if ref is None:
+                ref = check[i].clone()
+            elif not torch.equal(check[i], ref):
+                print(f"variant {i} {variants[i]} MISMATCH: {int((check[i] != ref).sum())} cells")
     times = [[] for _ in variants]
     for r in range(args.rounds):
         for i, (st, a) in enumerate(zip(stencils, argsets)):
