@@ -19,6 +19,7 @@ import time
 
 from gt4py_amd.backend.base import BaseBackend, register
 from gt4py_amd.codegen import hip as hipgen
+from gt4py_amd.codegen.lowering import lower_data_dims
 from gt4py_amd.codegen.plan import make_plan
 from gt4py_amd.runtime import jit
 from gt4py_amd.runtime.launcher import StencilLauncher
@@ -55,7 +56,7 @@ class Mi355xBackend(BaseBackend):
     name = "gt:mi355x"
     options = {
         "device_sync": {"versioning": False, "type": bool, "description": "synchronize the stream after each call"},
-        "jchunk": {"versioning": True, "type": int, "description": "J rows per wavefront in plane kernels"},
+        "jchunk": {"versioning": True, "type": int, "description": "J rows per wavefront in plane kernels (0 = auto)"},
         "vector": {"versioning": True, "type": int, "description": "I elements per lane in plane kernels (1, 2, 4)"},
         "prefetch": {"versioning": True, "type": int, "description": "rows loaded ahead in plane kernels"},
         "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
@@ -79,8 +80,11 @@ class Mi355xBackend(BaseBackend):
         b = self.builder
         opts = dict(b.options.backend_opts)
         t0 = time.perf_counter()
-        plan = make_plan(b.analysis)
-        source, signature = hipgen.generate(b.analysis, plan, opts)
+        analysis, components = lower_data_dims(b.analysis)
+        plan = make_plan(analysis)
+        source, signature = hipgen.generate(
+            analysis, plan, opts, abi_fields=b.analysis.stencil.field_params(), components=components
+        )
         t1 = time.perf_counter()
         path = jit.compile_source(source, verbose=bool(opts.get("verbose")))
         t2 = time.perf_counter()

@@ -215,10 +215,83 @@ class NumpyExecutor:
             out |= np.broadcast_to(rng(hm.i, ni, ii) & rng(hm.j, nj, jj), _shape(reg))
         return out
 
+    # -------------------------------------------------------------- data dims / run-time K offsets
+    def _index_scalar(self, e, reg):
+        v = self._ev(e, reg)
+        if isinstance(v, np.ndarray):
+            if v.size != 1 and not np.all(v == v.reshape(-1)[0]):
+                return v
+            v = v.reshape(-1)[0]
+        return int(v)
+
+    def _data_select(self, v, data_index, reg):
+        """``v[..., d0, d1, ...]`` for the trailing data dimensions of a field view."""
+        idx = [self._index_scalar(d, reg) for d in data_index]
+        if all(isinstance(x, int) for x in idx):
+            return v[(Ellipsis,) + tuple(idx)]
+        shp = _shape(reg)
+        lead = np.broadcast_to(v[(Ellipsis,) + (0,) * len(idx)], shp).shape
+        grids = list(np.indices(lead, sparse=True))
+        full = [np.broadcast_to(x, lead) if isinstance(x, np.ndarray) else x for x in idx]
+        return np.broadcast_to(v, lead + v.shape[v.ndim - len(idx):])[tuple(grids) + tuple(full)]
+
+    def _gather_index(self, e: ir.FieldAccess, f: "_Arr", reg):
+        """Fancy index of ``f.array`` for an access with a run-time K offset over ``reg``."""
+        i0, i1, j0, j1, k0, k1 = reg
+        di, dj, dk = e.offset
+        shp = _shape(reg)
+        ii = np.arange(i0 + di, i1 + di)[:, None, None] + f.origin[0]
+        jj = np.arange(j0 + dj, j1 + dj)[None, :, None] + f.origin[1]
+        kv = self._ev(e.k_offset, reg)
+        kk = np.arange(k0 + dk, k1 + dk)[None, None, :] + f.origin[2] + np.asarray(kv).astype(np.int64)
+        if f.mask[2]:
+            # out-of-range levels are clipped to the array (utils/field.py:53-57)
+            kk = np.clip(kk, 0, f.array.shape[sum(f.mask[:2])] - 1)
+        ii, jj, kk = (np.broadcast_to(x, shp) for x in (ii, jj, kk))
+        sel = [x for x, m in zip((ii, jj, kk), f.mask) if m]
+        for d in e.data_index:
+            sel.append(np.broadcast_to(np.asarray(self._ev(d, reg)).astype(np.int64), shp))
+        return tuple(sel)
+
+    def _assign_indexed(self, s: ir.Assign, reg, mask, value):
+        """Assignment whose target has a K offset, a run-time K offset or a data index."""
+        t = s.target
+        f = self.fields[t.name]
+        i0, i1, j0, j1, k0, k1 = reg
+        ni, nj, _ = self.domain
+        ci0, ci1, cj0, cj1 = max(i0, 0), min(i1, ni), max(j0, 0), min(j1, nj)
+        if ci1 <= ci0 or cj1 <= cj0:
+            return
+        sub = (slice(ci0 - i0, ci1 - i0), slice(cj0 - j0, cj1 - j0), slice(None))
+        creg = (ci0, ci1, cj0, cj1, k0, k1)
+        value = np.broadcast_to(value, _shape(reg))[sub]
+        if mask is not None:
+            mask = np.broadcast_to(mask, _shape(reg))[sub]
+        if t.k_offset is not None:
+            idx = self._gather_index(t, f, creg)
+        else:
+            dk = t.offset[2]
+            lo = [ci0 + f.origin[0], cj0 + f.origin[1], k0 + dk + f.origin[2]]
+            hi = [ci1 + f.origin[0], cj1 + f.origin[1], k1 + dk + f.origin[2]]
+            idx = [slice(a, b) for a, b, m in zip(lo, hi, f.mask) if m]
+            didx = [self._index_scalar(d, creg) for d in t.data_index]
+            if any(not isinstance(x, int) for x in didx):
+                raise NotImplementedError("field-valued data index in an assignment target")
+            idx = tuple(idx) + tuple(didx)
+        cur = f.array[idx]
+        val = np.broadcast_to(value, cur.shape) if cur.shape == value.shape or not all(f.mask) else value
+        if not all(f.mask):
+            val = np.broadcast_to(value, _shape(creg))[tuple(slice(None) if m else 0 for m in f.mask)]
+            if mask is not None:
+                mask = mask[tuple(slice(None) if m else 0 for m in f.mask)]
+        f.array[idx] = val if mask is None else np.where(mask, val, cur)
+
     def _assign(self, s: ir.Assign, reg, mask):
         name = s.target.name
         f = self.fields[name]
         value = self._ev(s.value, reg)
+        if s.target.k_offset is not None or s.target.offset[2] != 0 or s.target.data_index:
+            return self._assign_indexed(s, reg, mask, value)
         i0, i1, j0, j1, k0, k1 = reg
         if name in self.api:
             ni, nj, _ = self.domain
@@ -255,9 +328,14 @@ class NumpyExecutor:
             return self.scalars[e.name]
         if isinstance(e, ir.FieldAccess):
             f = self.fields[e.name]
+            if e.k_offset is not None:
+                return f.array[self._gather_index(e, f, reg)]
             di, dj, dk = e.offset
             i0, i1, j0, j1, k0, k1 = reg
-            return f.view(i0 + di, i1 + di, j0 + dj, j1 + dj, k0 + dk, k1 + dk)
+            v = f.view(i0 + di, i1 + di, j0 + dj, j1 + dj, k0 + dk, k1 + dk)
+            if e.data_index:
+                v = self._data_select(v, e.data_index, reg)
+            return v
         if isinstance(e, ir.Cast):
             v = self._ev(e.expr, reg)
             t = e.dtype.np_dtype

@@ -39,6 +39,8 @@ from gt4py_amd.passes import ZERO_EXTENT, StencilAnalysis, iter_accesses
 
 WAVE = 64
 PLANE_BLOCK_WAVES = 4
+PLANE_TARGET_BLOCKS = 60000  # auto J-chunk: aim for at least this many workgroups
+PLANE_MIN_JCHUNK = 4
 COLUMN_BLOCK = (64, 4)
 
 
@@ -192,6 +194,7 @@ class FieldSlot:
     index: int  # index in the gtmi_field array
     dtype: DataType
     is_scratch: bool
+    data_index: Tuple[str, ...] = ()  # host C expressions: component of a data-dimension field
 
     @property
     def c(self) -> str:
@@ -213,9 +216,13 @@ def host_fill(slot: FieldSlot, pvar: str, writable: bool) -> List[str]:
     t = slot.dtype.ctype
     cast = f"({t}*)" if writable else f"(const {t}*)"
     f = f"f[{slot.index}]"
+    comp = "".join(
+        f" + (int64_t)gtmi_clamp_index((int64_t)({x}), {f}.data_shape[{d}]) * {f}.data_strides[{d}]"
+        for d, x in enumerate(slot.data_index)
+    )
     return [
         f"{pvar}.p_{c} = {cast}{f}.data + ({f}.origin[0] * {f}.strides[0] + {f}.origin[1] * {f}.strides[1] + "
-        f"{f}.origin[2] * {f}.strides[2]);",
+        f"{f}.origin[2] * {f}.strides[2]{comp});",
         f"{pvar}.sI_{c} = {f}.strides[0]; {pvar}.sJ_{c} = {f}.strides[1]; {pvar}.sK_{c} = {f}.strides[2];",
         f"{pvar}.ilo_{c} = (int32_t)(-{f}.origin[0]); {pvar}.ihi_{c} = (int32_t)({f}.shape[0] - {f}.origin[0] - 1);",
         f"{pvar}.jlo_{c} = (int32_t)(-{f}.origin[1]); {pvar}.jhi_{c} = (int32_t)({f}.shape[1] - {f}.origin[1] - 1);",
@@ -737,8 +744,7 @@ class PlaneGen:
         for i_s, s in enumerate(self.st.scalar_params()):
             H.append(f"        memcpy(&p.s_{cname(s.name)}, &sc[{i_s}], sizeof(p.s_{cname(s.name)}));")
         H.append("        p.ni = ni; p.nj = nj; p.nk = nk; p.k0 = k0; p.nks = k1 - k0;")
-        H.append(f"        p.jc = {int(self.opts.get('jchunk', 32))};")
-        H.append("        p.n_chunks = (nj + p.jc - 1) / p.jc;")
+        jchunk = int(self.opts.get("jchunk", 0))
         vecs = sorted(launches, reverse=True)
         H.append("        int vsel = 1;")
         for V in vecs:
@@ -758,6 +764,18 @@ class PlaneGen:
             H.append(f"        {'if' if V == vecs[0] else 'else if'} (vsel == {V}) {{")
             H.append(f"            p.n_strips = (ni + {g['w_out']} - 1) / {g['w_out']};")
             H.append(f"            p.n_sgroups = (p.n_strips + {PLANE_BLOCK_WAVES - 1}) / {PLANE_BLOCK_WAVES};")
+            if jchunk > 0:
+                H.append(f"            p.jc = {jchunk};")
+            else:
+                # auto: the longest J chunk (<= 32 rows, >= 4) that still gives ~64K workgroups; shorter
+                # chunks trade halo-row re-reads for more concurrent row streams and a shorter tail
+                # (MI355X sweeps: hdiff 2048^2x160 best at 16, lap5 1024^2x80 at 4, hdiff f32 at 16)
+                H.append("            p.jc = 32;")
+                H.append(
+                    f"            while (p.jc > {PLANE_MIN_JCHUNK} && (long long)p.n_sgroups * ((nj + p.jc - 1) / p.jc) * "
+                    f"p.nks < {PLANE_TARGET_BLOCKS}LL) p.jc >>= 1;"
+                )
+            H.append("            p.n_chunks = (nj + p.jc - 1) / p.jc;")
             H.append("            const long long nblocks = (long long)p.n_sgroups * p.n_chunks * p.nks;")
             H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); return 2; }")
             H.append("            p.perm_a = gtmi_coprime_multiplier((long long)nblocks);")
@@ -923,9 +941,33 @@ class ColumnGen:
         self.opts = opts
         self.api = {p.name for p in self.st.field_params()}
         self.scratch = set(plan.scratch)
+        # compute region: the union of the IJ extents of the kernel's statements (temporaries that a
+        # later kernel reads at IJ offsets are produced on their halo too, passes.compute_extents)
+        ilo = ihi = jlo = jhi = 0
+        for li in kernel.loops:
+            for si, sec in enumerate(self.st.vertical_loops[li].sections):
+                for ti in range(len(sec.body)):
+                    (a, b), (c, d) = analysis.extents.blocks.get((li, si, ti), ((0, 0), (0, 0)))
+                    ilo, ihi, jlo, jhi = max(ilo, a), max(ihi, b), max(jlo, c), max(jhi, d)
+        self.ext = (ilo, ihi, jlo, jhi)
 
     def _mem(self, name):
         return name in self.api or name in self.scratch
+
+    def _guard(self, li, si, ti) -> Optional[str]:
+        """Condition restricting top-level statement ti to its own extent (None: whole region)."""
+        (a, b), (c, d) = self.a.extents.blocks.get((li, si, ti), ((0, 0), (0, 0)))
+        ilo, ihi, jlo, jhi = self.ext
+        conds = []
+        if a < ilo:
+            conds.append(f"i >= {-a}")
+        if b < ihi:
+            conds.append(f"i < p.ni + {b}")
+        if c < jlo:
+            conds.append(f"j >= {-c}")
+        if d < jhi:
+            conds.append(f"j < p.nj + {d}")
+        return " && ".join(conds) if conds else None
 
     def render(self) -> Tuple[str, str]:
         k = self.kid
@@ -977,9 +1019,10 @@ class ColumnGen:
             L.append("    extern __shared__ __attribute__((aligned(16))) char gtmi_lds_reserve[];")
             L.append("    if (p.ni < 0) gtmi_lds_reserve[threadIdx.x] = 0;  // keep the reservation alive")
         B = []
-        B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x);")
-        B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y);")
-        B.append("if (i >= p.ni || j >= p.nj) return;")
+        eilo, eihi, ejlo, ejhi = self.ext
+        B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x) - {eilo};")
+        B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y) - {ejlo};")
+        B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
         B.append("const int nk = p.nk;")
         for s in scalars:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
@@ -1000,8 +1043,8 @@ class ColumnGen:
         # resident columns small enough to be re-read from the 256 MiB Infinity Cache
         lds = 0 if occ <= 0 else min(160 * 1024, (160 * 1024) // occ - 1024)
         H.append(
-            f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {bx - 1}) / {bx}), "
-            f"(unsigned)((nj + {by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
+            f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
+            f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
         )
         H.append("    }")
         H.append("}")
@@ -1011,12 +1054,22 @@ class ColumnGen:
         vl = self.st.vertical_loops[li]
         order = vl.loop_order
         fwd = order != ir.LoopOrder.BACKWARD
+        # direct fields: read at a run-time K offset or written at a K offset in this loop; every
+        # access to them goes to memory at its own address (no register window)
+        direct: Set[str] = set()
+        for sec in vl.sections:
+            for acc, w in iter_accesses(sec.body):
+                if isinstance(acc, ir.FieldAccess) and (acc.k_offset is not None or (w and acc.offset[2] != 0)):
+                    if not self._mem(acc.name):
+                        raise UnsupportedStencil(f"run-time or written K offset on temporary '{acc.name}'")
+                    direct.add(acc.name)
+        self.direct = direct
         # windows: key (name, di, dj) -> [dmin, dmax]
         win: Dict[Tuple[str, int, int], List[int]] = {}
         wnames: Set[str] = set()
         for sec in vl.sections:
             for acc, w in iter_accesses(sec.body):
-                if not isinstance(acc, ir.FieldAccess):
+                if not isinstance(acc, ir.FieldAccess) or acc.name in direct:
                     continue
                 di, dj, dk = acc.offset
                 key = (acc.name, di, dj)
@@ -1034,6 +1087,8 @@ class ColumnGen:
         decl_dtype = {}
         for (name, di, dj) in win:
             decl_dtype[name] = self.st.decl(name).dtype
+        for name in direct:
+            decl_dtype[name] = self.st.decl(name).dtype
 
         def wvar(name, di, dj, d):
             rng = win[(name, di, dj)]
@@ -1049,11 +1104,11 @@ class ColumnGen:
 
         def mem_index(name, di, dj, kexpr):
             """A load expression (non-temporal for read-once streams)."""
-            nt = "true" if name in self.nt_loads else "false"
+            nt = "true" if (name in self.nt_loads and name not in direct) else "false"
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
 
         def mem_store(name, kexpr, value):
-            nt = "true" if name in self.nt_stores else "false"
+            nt = "true" if (name in self.nt_stores and name not in direct) else "false"
             return f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
 
         P = int(self.opts.get("kprefetch", 0))
@@ -1148,13 +1203,26 @@ class ColumnGen:
             body.append("}")
             body.append(f"k_next = k {step} 1;")
 
+            def kaddr(acc: ir.FieldAccess) -> str:
+                kexpr = f"k + ({acc.offset[2]})"
+                if acc.k_offset is not None:
+                    kexpr += f" + (int)({rend(acc.k_offset)})"
+                return kexpr
+
             def resolve(acc: ir.FieldAccess) -> str:
                 di, dj, dk = acc.offset
+                if acc.name in direct:
+                    return mem_index(acc.name, di, dj, kaddr(acc))
                 return wvar(acc.name, di, dj, dk)
 
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
-            for s in sec.body:
-                body += self._stmt(s, rend, wvar, mem_store)
+            self._kaddr = kaddr
+            for ti, s in enumerate(sec.body):
+                code = self._stmt(s, rend, wvar, mem_store)
+                g = self._guard(li, si, ti)
+                if g:
+                    code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
+                body += code
             out += ["            " + x for x in body]
             out.append("        }")
             out.append("    }")
@@ -1165,10 +1233,18 @@ class ColumnGen:
         mem_index = mem_store
         if isinstance(s, ir.Assign):
             name = s.target.name
+            if name in self.direct:
+                st = mem_store(name, self._kaddr(s.target), rend(s.value))
+                if name in self.api and any(self.ext):
+                    st = f"if (i >= 0 && i < p.ni && j >= 0 && j < p.nj) {st}"
+                return [st]
             tgt = wvar(name, 0, 0, 0)
             out = [f"{tgt} = {rend(s.value)};"]
             if self._mem(name):
-                out.append(mem_store(name, "k", tgt))
+                st = mem_store(name, "k", tgt)
+                if name in self.api and any(self.ext):
+                    st = f"if (i >= 0 && i < p.ni && j >= 0 && j < p.nj) {st}"
+                out.append(st)
             return out
         if isinstance(s, ir.If):
             out = [f"if ({rend(s.cond)}) {{"]
@@ -1205,12 +1281,22 @@ def _sgn(x: int) -> str:
 # ------------------------------------------------------------------------------------------
 
 
-def generate(analysis: StencilAnalysis, plan: KernelPlan, opts: Dict) -> Tuple[str, Dict]:
+def generate(
+    analysis: StencilAnalysis, plan: KernelPlan, opts: Dict, abi_fields=None, components=None
+) -> Tuple[str, Dict]:
+    """``abi_fields``: the API field declarations in ABI order (default: the stencil's);
+    ``components``: data-dimension components from ``lowering.lower_data_dims``."""
     st = analysis.stencil
+    components = components or {}
+    abi_fields = list(abi_fields) if abi_fields is not None else st.field_params()
     slots: Dict[str, FieldSlot] = {}
     idx = 0
-    for p in st.field_params():
+    host_scalar = ExprRenderer(lambda acc: "0", lambda n: f"hs_{cname(n)}", lambda ax: "0")
+    for p in abi_fields:
         slots[p.name] = FieldSlot(p.name, idx, p.dtype, False)
+        for vname, comp in components.items():
+            if comp.base == p.name:
+                slots[vname] = FieldSlot(vname, idx, p.dtype, False, tuple(host_scalar(x) for x in comp.index))
         idx += 1
     for t in plan.scratch:
         slots[t] = FieldSlot(t, idx, st.decl(t).dtype, True)
@@ -1228,9 +1314,10 @@ def generate(analysis: StencilAnalysis, plan: KernelPlan, opts: Dict) -> Tuple[s
     import json
 
     signature = {
-        "abi": 1,
+        "abi": 2,
         "fields": [
-            {"name": p.name, "dtype": p.dtype.name.lower(), "axes": list(p.axes)} for p in st.field_params()
+            {"name": p.name, "dtype": p.dtype.name.lower(), "axes": list(p.axes), "data_dims": list(p.data_dims)}
+            for p in abi_fields
         ],
         "scratch": [
             {"name": t, "dtype": st.decl(t).dtype.name.lower(), "extent": [list(e) for e in plan.scratch_extent[t]]}
@@ -1241,6 +1328,11 @@ def generate(analysis: StencilAnalysis, plan: KernelPlan, opts: Dict) -> Tuple[s
     }
     sig_json = json.dumps(signature).replace("\\", "\\\\").replace('"', '\\"')
     n_scalars = len(st.scalar_params())
+    host_scalars = [
+        f"    {sp.dtype.ctype} hs_{cname(sp.name)}; memcpy(&hs_{cname(sp.name)}, &sc[{i}], sizeof(hs_{cname(sp.name)})); "
+        f"(void)hs_{cname(sp.name)};"
+        for i, sp in enumerate(st.scalar_params())
+    ]
     src = f"""// Generated by gt4py_amd (gt:mi355x). Do not edit.
 #include "gtmi_device.h"
 #include "gtmi.h"
@@ -1268,6 +1360,7 @@ extern "C" int gtmi_stencil_run(const int64_t* domain, const gtmi_field* f, int3
     hipStream_t stream = (hipStream_t)stream_ptr;
     const int ni = (int)domain[0], nj = (int)domain[1], nk = (int)domain[2];
     (void)ni; (void)nj; (void)nk;
+{chr(10).join(host_scalars)}
 {chr(10).join("    " + line for h in launches for line in h.splitlines())}
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {{

@@ -87,6 +87,8 @@ def make_plan(analysis: StencilAnalysis) -> KernelPlan:
 
     for li, vl in enumerate(st.vertical_loops):
         if vl.loop_order == ir.LoopOrder.PARALLEL and _has_horizontal_offsets(vl):
+            if any(isinstance(a, ir.FieldAccess) and a.k_offset is not None for a, _ in _loop_accesses(vl)):
+                raise UnsupportedStencil("run-time K offsets in a PARALLEL computation with horizontal offsets")
             flush()
             for si in range(len(vl.sections)):
                 kernels.append(PlaneKernel(li, si))

@@ -13,6 +13,9 @@
 
 #define GTMI_DEV __device__ __forceinline__
 
+// host side: a data-dimension index clamped into [0, n) (no out-of-bounds component pointer)
+static inline int64_t gtmi_clamp_index(int64_t x, int64_t n) { return x < 0 ? 0 : (x >= n ? n - 1 : x); }
+
 namespace gtmi {
 
 // ---------------------------------------------------------------- wave shuffles (wave64)

@@ -31,6 +31,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from gt4py_amd import ir
+from gt4py_amd.gtscript import Axis
 from gt4py_amd.ir import DataType
 
 _GTSCRIPT_FUNC_ATTR = "__gtscript_function__"
@@ -310,6 +311,7 @@ class StencilParser:
         if self._call_name(first) != "computation":
             raise GTScriptSyntaxError("Expected 'with computation(...)'")
         order = self._parse_order(first, scope)
+        self._loop_order = order
         sections: List[ir.Section] = []
         if len(items) == 2:
             second = items[1].context_expr
@@ -463,13 +465,32 @@ class StencilParser:
         return pre + self._assign_to(target, val, scope)
 
     def _assign_to(self, target, val: ir.Expr, scope: _Scope) -> List[ir.Stmt]:
+        pre: List[ir.Stmt] = []
+        t_off = (0, 0, 0)
+        t_didx = None
         if isinstance(target, ast.Subscript):
             base = target.value
+            if isinstance(base, ast.Subscript) and isinstance(base.value, ast.Name):
+                t_didx = self._parse_data_index(target.slice, scope, pre)
+                target = base
+                base = target.value
             if not isinstance(base, ast.Name):
                 raise GTScriptSyntaxError("Invalid assignment target")
-            offs = self._parse_offset(target.slice, scope)
-            if any(offs):
-                raise GTScriptSyntaxError(f"Assignment to '{base.id}' with non-zero offset {offs}")
+            offs = self._parse_offset(target.slice, scope, pre)
+            if isinstance(offs, tuple) and len(offs) == 2 and offs[0] == "axes":
+                offs = offs[1]
+            decl = self._decl_of(base.id, scope)
+            if decl is not None and base.id in self.fields and len(offs) == sum(decl.mask) and len(offs) != 3:
+                it = iter(offs)
+                offs = tuple(next(it) if m else 0 for m in decl.mask)
+            if len(offs) == 3:
+                if any(isinstance(o, ir.Expr) or o != 0 for o in offs[:2]):
+                    raise GTScriptSyntaxError("Assignment to non-zero offsets is not supported in IJ.")
+                if (isinstance(offs[2], ir.Expr) or offs[2] != 0) and getattr(self, "_loop_order", None) == ir.LoopOrder.PARALLEL:
+                    raise GTScriptSyntaxError(
+                        "Assignment to non-zero offsets in K is not available in PARALLEL. Choose FORWARD or BACKWARD."
+                    )
+            t_off = offs
             target = base
         if not isinstance(target, ast.Name):
             raise GTScriptSyntaxError("Invalid assignment target")
@@ -487,41 +508,134 @@ class StencilParser:
         else:
             name_res = self._temp_for_local(name, scope, create=True)
             if name_res not in self.temporaries:
+                if t_didx:
+                    raise GTScriptSyntaxError("Temporaries with data dimensions need to be declared explicitly.")
                 self.temporaries[name_res] = ir.FieldDecl(name_res, DataType.AUTO, is_temporary=True)
-        return [ir.Assign(ir.FieldAccess(name_res, (0, 0, 0)), val)]
+        if t_off != (0, 0, 0) or t_didx:
+            tgt = self._field_access(name_res, t_off, scope, t_didx)
+            if tgt.offset[2] != 0 or tgt.k_offset is not None:
+                if name_res not in self.fields:
+                    raise GTScriptSyntaxError("Assignment with a K offset is only supported for API fields")
+        else:
+            tgt = ir.FieldAccess(name_res, (0, 0, 0))
+        return pre + [ir.Assign(tgt, val)]
 
     # ------------------------------------------------------------------ expressions
-    def _parse_offset(self, sl, scope) -> Tuple[int, int, int]:
+    def _parse_offset(self, sl, scope, pre=None) -> Tuple:
+        """Spatial index of a subscript: ints, or (K only) a run-time integer expression.
+
+        Accepts ``[1, 0, -1]``, ``[0, 0, lev + 1]`` and the axis form ``[I - 1]`` / ``[K + 1]``
+        (reference ``gtscript_frontend.py:1316-1390``); the axis form returns all three offsets.
+        """
         elts = sl.elts if isinstance(sl, ast.Tuple) else [sl]
-        vals = [int(self._const_eval(e, scope)) for e in elts]
+        axis_form = any(
+            isinstance(n, ast.Name) and n.id in ("I", "J", "K") and isinstance(self._try_const(n, scope), Axis)
+            for e in elts
+            for n in ast.walk(e)
+        )
+        if axis_form:
+            off = [0, 0, 0]
+            for e in elts:
+                shift = 0
+                node = e
+                if isinstance(e, ast.BinOp) and isinstance(e.op, (ast.Add, ast.Sub)):
+                    shift = int(self._const_eval(e.right, scope)) * (1 if isinstance(e.op, ast.Add) else -1)
+                    node = e.left
+                ax = self._try_const(node, scope)
+                if not isinstance(ax, Axis):
+                    raise GTScriptSyntaxError("Invalid axis offset expression")
+                off["IJK".index(ax.name)] = shift
+            return ("axes", tuple(off))
+        vals = []
+        for e in elts:
+            v = self._try_const(e, scope)
+            if isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_)):
+                vals.append(int(v))
+            elif pre is None:
+                raise GTScriptSyntaxError("Run-time offsets are only allowed in expressions and assignment targets")
+            else:
+                vals.append(self._parse_expr(e, scope, pre))
         return tuple(vals)
 
-    def _field_access(self, name: str, offset, scope) -> ir.FieldAccess:
+    def _decl_of(self, name: str, scope: _Scope):
+        """FieldDecl a (possibly aliased) name refers to, or None."""
+        if name in scope.aliases:
+            alias = scope.aliases[name]
+            if isinstance(alias, tuple) and alias[0] == "field":
+                name = alias[1]
+            else:
+                return None
+        elif name in scope.locals:
+            name = scope.locals[name]
+        return self.fields.get(name) or self.temporaries.get(name)
+
+    def _try_const(self, node, scope):
+        try:
+            return self._const_eval(node, scope)
+        except Exception:  # noqa: BLE001 - not a compile-time value
+            return None
+
+    def _parse_data_index(self, sl, scope, pre) -> List[ir.Expr]:
+        elts = sl.elts if isinstance(sl, ast.Tuple) else [sl]
+        out = []
+        for e in elts:
+            v = self._try_const(e, scope)
+            if isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_)):
+                out.append(ir.Literal(int(v), DataType.INT32))
+            else:
+                out.append(self._parse_expr(e, scope, pre))
+        return out
+
+    def _field_access(self, name: str, offset, scope, data_index=None) -> ir.FieldAccess:
         decl = self.fields.get(name) or self.temporaries.get(name)
-        off = list(offset)
-        if decl is not None and name in self.fields:
-            mask = decl.mask
-            if len(off) == sum(mask) and len(off) != 3:
-                it = iter(off)
-                off = [next(it) if m else 0 for m in mask]
+        if isinstance(offset, tuple) and len(offset) == 2 and offset[0] == "axes":
+            off = list(offset[1])
+        else:
+            off = list(offset)
+            if decl is not None and name in self.fields:
+                mask = decl.mask
+                if len(off) == sum(mask) and len(off) != 3:
+                    it = iter(off)
+                    off = [next(it) if m else 0 for m in mask]
         if len(off) != 3:
             raise GTScriptSyntaxError(f"Invalid offset {tuple(offset)} for '{name}'")
-        return ir.FieldAccess(name, tuple(off))
+        k_expr = None
+        if isinstance(off[2], ir.Expr):
+            k_expr, off[2] = off[2], 0
+        if any(isinstance(o, ir.Expr) for o in off[:2]):
+            raise GTScriptSyntaxError(f"Run-time offsets are only supported along K ('{name}')")
+        ndd = len(decl.data_dims) if decl is not None else 0
+        data_index = list(data_index or [])
+        if len(data_index) != ndd:
+            raise GTScriptSyntaxError(
+                f"Incorrect data index length {len(data_index)}. Invalid data dimension index. "
+                f"Field {name} has {ndd} data dimensions."
+            )
+        for d, n in zip(data_index, decl.data_dims if decl is not None else ()):
+            if isinstance(d, ir.Literal) and not (0 <= int(d.value) < n):
+                raise GTScriptSyntaxError(f"Data index out of bounds for field {name}")
+        return ir.FieldAccess(name, tuple(off), data_index=data_index, k_offset=k_expr)
 
-    def _resolve_name(self, name: str, scope: _Scope, offset=(0, 0, 0)) -> ir.Expr:
+    def _resolve_name(self, name: str, scope: _Scope, offset=(0, 0, 0), data_index=None) -> ir.Expr:
+        if isinstance(offset, tuple) and len(offset) == 2 and offset[0] == "axes":
+            offset = offset[1]
         if name in scope.aliases:
             alias = scope.aliases[name]
             if isinstance(alias, tuple) and alias[0] == "field":
                 base_off = alias[2]
-                return self._field_access(alias[1], tuple(a + b for a, b in zip(base_off, offset)), scope)
-            if any(offset):
+                off = tuple(
+                    (a + b) if not isinstance(b, ir.Expr) else (b if a == 0 else ir.BinaryOp("+", b, ir.Literal(a, DataType.INT64)))
+                    for a, b in zip(base_off, offset)
+                )
+                return self._field_access(alias[1], off, scope, data_index)
+            if any(not isinstance(o, int) or o for o in offset):
                 raise GTScriptSyntaxError(f"Offset access to non-field argument '{name}'")
             return alias
         if name in scope.locals:
-            return ir.FieldAccess(scope.locals[name], tuple(offset))
+            return self._field_access(scope.locals[name], tuple(offset), scope, data_index)
         if scope is self._root_scope:
             if name in self.fields:
-                return self._field_access(name, offset, scope)
+                return self._field_access(name, offset, scope, data_index)
             if name in self.scalars:
                 if any(offset):
                     raise GTScriptSyntaxError(f"Offset access to scalar '{name}'")
@@ -546,10 +660,27 @@ class StencilParser:
             return self._resolve_name(node.id, scope)
         if isinstance(node, ast.Subscript):
             if isinstance(node.value, ast.Name):
-                offs = self._parse_offset(node.slice, scope)
+                decl = self._decl_of(node.value.id, scope)
+                if decl is not None and decl.data_dims and not any(decl.mask):
+                    raise GTScriptSyntaxError(
+                        f"Incorrect offset specification detected for {node.value.id}. "
+                        f"Did you mean absolute indexing via .A[...]?"
+                    )
+                offs = self._parse_offset(node.slice, scope, pre)
                 return self._resolve_name(node.value.id, scope, offs)
-            if isinstance(node.value, ast.Subscript):
-                raise GTScriptSyntaxError("Data-dimension indexing is not supported yet")
+            if isinstance(node.value, ast.Subscript) and isinstance(node.value.value, ast.Name):
+                # f[i, j, k][d0, d1, ...]: data-dimension index
+                offs = self._parse_offset(node.value.slice, scope, pre)
+                didx = self._parse_data_index(node.slice, scope, pre)
+                return self._resolve_name(node.value.value.id, scope, offs, didx)
+            if (
+                isinstance(node.value, ast.Attribute)
+                and node.value.attr == "A"
+                and isinstance(node.value.value, ast.Name)
+            ):
+                # table.A[d0, ...]: absolute data index at the current point (GlobalTable)
+                didx = self._parse_data_index(node.slice, scope, pre)
+                return self._resolve_name(node.value.value.id, scope, (0, 0, 0), didx)
             raise GTScriptSyntaxError("Invalid subscript")
         if isinstance(node, ast.Attribute):
             v = self._const_eval(node, scope)

@@ -30,6 +30,7 @@ __all__ = [
     "FORWARD",
     "BACKWARD",
     "Field",
+    "GlobalTable",
     "computation",
     "interval",
     "horizontal",
@@ -174,6 +175,20 @@ class _FieldDescriptorMaker:
 
 
 Field = _FieldDescriptorMaker()
+
+
+class _TableDescriptorMaker:
+    """``GlobalTable[(dtype, (n0, n1, ...))]``: data dimensions only, read with ``table.A[...]``
+    (reference ``gtscript.py:734-749``)."""
+
+    def __getitem__(self, spec):
+        if not isinstance(spec, collections.abc.Collection) or len(spec) != 2:
+            raise ValueError("GlobalTable is defined by a tuple (type, [axes_size..])")
+        dtype, data_dims = spec
+        return _FieldDescriptor(dtype, [], data_dims)
+
+
+GlobalTable = _TableDescriptorMaker()
 
 # --------------------------------------------------------------------------------------
 # Context managers / markers (bodies are parsed, never executed)

@@ -168,12 +168,23 @@ class Literal(Expr):
 
 @dataclasses.dataclass(eq=True)
 class FieldAccess(Expr):
-    """Access to an API field or temporary at a relative offset (I, J, K)."""
+    """Access to an API field or temporary at a relative offset (I, J, K).
+
+    ``data_index``: one integer expression per data dimension of the field (``f[0, 0, 0][i]``,
+    ``table.A[i, j]``; ``gtir.FieldAccess.data_index``). ``k_offset``: a run-time vertical offset
+    added to ``offset[2]`` (``f[0, 0, lev]``; ``gtc/common.py:341-351`` VariableKOffset).
+    """
 
     name: str
     offset: Tuple[int, int, int]
     dtype: DataType = DataType.AUTO
-    data_index: Tuple[int, ...] = ()
+    data_index: List[Expr] = dataclasses.field(default_factory=list)
+    k_offset: Optional[Expr] = None
+
+    @property
+    def is_direct(self) -> bool:
+        """Needs an address computed at run time (cannot live in a register ring/window)."""
+        return self.k_offset is not None
 
 
 @dataclasses.dataclass(eq=True)

@@ -97,7 +97,10 @@ def resolve_dtypes(stencil: ir.Stencil) -> ir.Stencil:
                 if getattr(d, "is_temporary", False) and name not in temp_dtype:
                     temp_dtype[name] = value.dtype
                 tgt = dataclasses.replace(
-                    s.target, dtype=temp_dtype[name] if getattr(d, "is_temporary", False) else d.dtype
+                    s.target,
+                    dtype=temp_dtype[name] if getattr(d, "is_temporary", False) else d.dtype,
+                    data_index=[ir.map_expr(x, type_expr) for x in s.target.data_index],
+                    k_offset=None if s.target.k_offset is None else ir.map_expr(s.target.k_offset, type_expr),
                 )
                 out.append(ir.Assign(tgt, value))
             elif isinstance(s, ir.If):
@@ -248,6 +251,12 @@ def _upcast_expr(e: ir.Expr) -> ir.Expr:
         return _retype(ir.NativeCall(e.func, [_cast(t, a) for t, a in zip(targets, args)]))
     if isinstance(e, ir.Cast):
         return ir.Cast(e.dtype, _upcast_expr(e.expr))
+    if isinstance(e, ir.FieldAccess) and (e.data_index or e.k_offset is not None):
+        return dataclasses.replace(
+            e,
+            data_index=[_upcast_expr(x) for x in e.data_index],
+            k_offset=None if e.k_offset is None else _upcast_expr(e.k_offset),
+        )
     return e
 
 
@@ -257,7 +266,7 @@ def upcast(stencil: ir.Stencil) -> ir.Stencil:
         for s in stmts:
             if isinstance(s, ir.Assign):
                 v = _upcast_expr(s.value)
-                out.append(ir.Assign(s.target, _cast(s.target.dtype, v)))
+                out.append(ir.Assign(_upcast_expr(s.target), _cast(s.target.dtype, v)))
             elif isinstance(s, ir.If):
                 out.append(ir.If(_upcast_expr(s.cond), visit_stmts(s.body), visit_stmts(s.orelse)))
             elif isinstance(s, ir.While):
@@ -304,6 +313,8 @@ def iter_accesses(stmts):
     def visit(s):
         if isinstance(s, ir.Assign):
             yield from expr_accesses(s.value)
+            for sub in list(s.target.data_index) + ([s.target.k_offset] if s.target.k_offset is not None else []):
+                yield from expr_accesses(sub)
             yield s.target, True
         elif isinstance(s, ir.If):
             yield from expr_accesses(s.cond)
@@ -390,16 +401,28 @@ def compute_extents(stencil: ir.Stencil) -> ExtentInfo:
 # --------------------------------------------------------------------------------------
 
 
+def _outer_field_accesses(stmts):
+    """FieldAccess nodes that are not nested in another access's run-time offset or data index
+    (the reference's KBoundaryVisitor does not descend into a visited FieldAccess)."""
+    stack = list(reversed(list(stmts)))
+    while stack:
+        n = stack.pop()
+        if isinstance(n, ir.FieldAccess):
+            yield n
+            continue
+        stack.extend(reversed(list(ir.iter_children(n))))
+
+
 def compute_k_boundary(stencil: ir.Stencil) -> Dict[str, Tuple[int, int]]:
     temps = {t.name for t in stencil.temporaries}
     bounds: Dict[str, List[float]] = {}
     for vl in stencil.vertical_loops:
         for sec in vl.sections:
             itv = sec.interval
-            for acc, _ in iter_accesses(sec.body):
-                if not isinstance(acc, ir.FieldAccess):
-                    continue
+            for acc in _outer_field_accesses(sec.body):
                 b = bounds.setdefault(acc.name, [-math.inf, -math.inf])
+                if acc.k_offset is not None:
+                    continue  # run-time offsets do not enter the boundary (gtir_k_boundary.py:55)
                 k = acc.offset[2]
                 if itv.start.level == ir.LevelMarker.START:
                     b[0] = max(-itv.start.offset - k, b[0])

@@ -12,7 +12,7 @@ import json
 import threading
 from typing import Dict
 
-GTMI_ABI_VERSION = 1
+GTMI_ABI_VERSION = 2
 
 DTYPE_IDS = {
     "bool": 10,
@@ -25,6 +25,9 @@ DTYPE_IDS = {
 }
 
 
+MAX_DATA_DIMS = 4  # GTMI_MAX_DATA_DIMS
+
+
 class GtmiField(ctypes.Structure):
     _fields_ = [
         ("data", ctypes.c_void_p),
@@ -33,6 +36,10 @@ class GtmiField(ctypes.Structure):
         ("shape", ctypes.c_int64 * 3),
         ("dtype", ctypes.c_int32),
         ("ndim", ctypes.c_int32),
+        ("n_data_dims", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("data_strides", ctypes.c_int64 * MAX_DATA_DIMS),
+        ("data_shape", ctypes.c_int64 * MAX_DATA_DIMS),
     ]
 
 

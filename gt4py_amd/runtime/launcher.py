@@ -106,10 +106,20 @@ class StencilLauncher:
                 raise TypeError(f"The dtype of field '{name}' is '{got}' instead of '{want}'")
             org = origin[name]
             axes = decl["axes"]
+            ddims = decl.get("data_dims", [])
             st = t.stride()
             sh = t.shape
-            if len(sh) != len(axes):
-                raise ValueError(f"Storage for '{name}' has {len(sh)} dimensions, expected {len(axes)} ({axes})")
+            if len(sh) != len(axes) + len(ddims):
+                raise ValueError(
+                    f"Storage for '{name}' has {len(sh)} dimensions, expected {len(axes) + len(ddims)} "
+                    f"({axes} + data dimensions {ddims})"
+                )
+            if len(ddims) > ffi.MAX_DATA_DIMS:
+                raise ValueError(f"'{name}': at most {ffi.MAX_DATA_DIMS} data dimensions are supported")
+            f.n_data_dims = len(ddims)
+            for d in range(len(ddims)):
+                f.data_strides[d] = st[len(axes) + d]
+                f.data_shape[d] = sh[len(axes) + d]
             d = 0
             for ax in range(3):
                 if _AXES[ax] in axes:

@@ -43,18 +43,20 @@ def _error_on_invalid_preset(backend):
 
 
 def _normalize_spec(aligned_index, shape, dtype, dimensions):
+    """Validate the spec; a subarray dtype appends its shape as trailing data dimensions
+    (aligned index 0 there), as ``storage/cartesian/utils.py:84-170`` does."""
     if not isinstance(shape, (tuple, list)) or not all(isinstance(s, numbers.Integral) for s in shape):
         raise TypeError("shape must be a sequence of integers")
     shape = tuple(int(s) for s in shape)
-    dtype = np.dtype(dtype)
-    if dtype.shape:
-        shape = shape + tuple(dtype.shape)
-        dtype = dtype.base
     if dimensions is None:
         dimensions = ("I", "J", "K")[: min(3, len(shape))] + tuple(str(d) for d in range(len(shape) - 3))
-    dimensions = tuple(str(d) for d in dimensions)
+    dimensions = tuple(str(getattr(d, "__gt_axis_name__", d)) for d in dimensions)
+    if not all(d.isdigit() or d in ("I", "J", "K") for d in dimensions):
+        raise ValueError(f"Invalid dimensions definition: '{dimensions}'")
     if len(dimensions) != len(shape):
         raise ValueError(f"dimensions {dimensions} do not match shape {shape}")
+    if any(s <= 0 for s in shape):
+        raise ValueError(f"shape ({shape}) contains non-positive value.")
     if aligned_index is None:
         aligned_index = (0,) * len(shape)
     aligned_index = tuple(int(a) for a in aligned_index)
@@ -62,6 +64,13 @@ def _normalize_spec(aligned_index, shape, dtype, dimensions):
         raise ValueError("aligned_index must have one entry per dimension")
     if any(a < 0 for a in aligned_index):
         raise ValueError("aligned_index must be non-negative")
+    dtype = np.dtype(dtype)
+    if dtype.shape:
+        sub = tuple(dtype.shape)
+        shape = shape + sub
+        aligned_index = aligned_index + (0,) * len(sub)
+        dimensions = dimensions + tuple(str(d) for d in range(len(sub)))
+        dtype = dtype.base
     return aligned_index, shape, dtype, dimensions
 
 

@@ -13,7 +13,7 @@
  *       pyext_module.run_computation(list(_domain_), field, list(_origin_["field"]), ..., exec_info)
  *
  * Mapping: `domain` -> domain[3]; every (field, origin) pair -> one gtmi_field (borrowed device
- * pointer, per-axis element strides, origin, shape); scalars -> gtmi_scalar slots in the
+ * pointer, per-axis element strides, origin, shape, data-dimension strides/extents); scalars -> gtmi_scalar slots in the
  * stencil's parameter order (gtir.params order, gtc_common.py:148-163); the CUDA/HIP stream
  * (the reference syncs with cupy, gtc_common.py:288-296) -> `stream`. exec_info timing stays
  * on the Python side (run_cpp_start_time / run_cpp_end_time around the call).
@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define GTMI_ABI_VERSION 1
+#define GTMI_ABI_VERSION 2
+#define GTMI_MAX_DATA_DIMS 4
 
 /* dtype ids = gt4py DataType ids (gtc/common.py:105-118) */
 enum gtmi_dtype {
@@ -53,6 +54,10 @@ typedef struct gtmi_field {
     int64_t shape[3];    /* array extent along I, J, K (1 for an absent axis) */
     int32_t dtype;       /* enum gtmi_dtype */
     int32_t ndim;        /* number of spatial axes the field has */
+    int32_t n_data_dims; /* trailing data dimensions (Field[(dtype, (n, ...))], GlobalTable) */
+    int32_t reserved;
+    int64_t data_strides[GTMI_MAX_DATA_DIMS]; /* element strides of the data dimensions */
+    int64_t data_shape[GTMI_MAX_DATA_DIMS];   /* their extents (indices are clamped to them) */
 } gtmi_field;
 
 typedef union gtmi_scalar {

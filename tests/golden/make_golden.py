@@ -47,6 +47,10 @@ def main(selected=None):
     import stencil_cases as sc  # noqa: E402
 
     manifest = {}
+    mpath = os.path.join(HERE, "manifest.json")
+    if selected and os.path.exists(mpath):
+        with open(mpath) as f:
+            manifest = json.load(f)
     for name, case in sc.CASES.items():
         if selected and name not in selected:
             continue
@@ -102,7 +106,7 @@ def main(selected=None):
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **payload)
         manifest[name] = {"seed": case.seed, **meta}
         print(f"[ok]   {name}")
-    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+    with open(mpath, "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 
 

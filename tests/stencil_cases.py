@@ -130,6 +130,13 @@ def _make_array(spec: FieldSpec, rng: np.random.Generator) -> np.ndarray:
         arr = rng.uniform(init[1], init[2], size=shape)
     elif isinstance(init, tuple) and init[0] == "int":
         arr = rng.integers(init[1], init[2], size=shape)
+    elif isinstance(init, tuple) and init[0] == "ramp":
+        # monotone along the last spatial axis (pressure-like columns), jittered across I/J
+        nk = shape[2] if len(shape) >= 3 else shape[-1]
+        kk = np.arange(nk) / max(nk - 1, 1)
+        base = init[1] + (init[2] - init[1]) * kk
+        jit = rng.uniform(0.0, 0.2 * (init[2] - init[1]) / max(nk, 1), size=shape[:2] + (1,) if len(shape) >= 3 else (1,))
+        arr = np.broadcast_to(base + jit, shape).copy()
     elif isinstance(init, tuple) and init[0] == "const":
         arr = np.full(shape, init[1])
     else:
@@ -1155,3 +1162,401 @@ case(
     origin={"a": (2, 2, 0), "out": (0, 0, 0)},
     domain=(11, 9, 4),
 )(multi_stage_temps)
+
+
+# --------------------------------------------------------------------------------------
+# Temporaries produced by a column kernel on an IJ halo, lower-dimensional fields
+# (test_code_generation.py:171-307, 868-891)
+# --------------------------------------------------------------------------------------
+
+
+def column_temp_halo(a: F64, out: F64):
+    with computation(PARALLEL):
+        with interval(0, -1):
+            tmp = a[0, 0, 1] * 2.0 - a
+        with interval(-1, None):
+            tmp = a
+    with computation(PARALLEL), interval(...):
+        out = tmp[1, 0, 0] - tmp[-1, 0, 0] + tmp[0, 1, 0] * tmp[0, -1, 0]
+
+
+case(
+    "column_temp_halo",
+    fields={"a": fs(12, 11, 6), "out": fs(10, 9, 6, init="zeros")},
+    origin={"a": (1, 1, 0), "out": (0, 0, 0)},
+    domain=(10, 9, 6),
+)(column_temp_halo)
+
+
+def forward_temp_halo(a: F64, out: F64):
+    with computation(FORWARD):
+        with interval(0, 1):
+            acc = a
+        with interval(1, None):
+            acc = acc[0, 0, -1] * 0.5 + a
+    with computation(PARALLEL), interval(...):
+        out = acc[1, 0, 0] + acc[0, -1, 0] - acc[-1, 1, 0]
+
+
+case(
+    "forward_temp_halo",
+    fields={"a": fs(12, 11, 7), "out": fs(10, 9, 7, init="zeros")},
+    origin={"a": (1, 1, 0), "out": (0, 0, 0)},
+    domain=(10, 9, 7),
+)(forward_temp_halo)
+
+
+F1DK = Field[gtscript.K, np.float64]
+F3D = Field[gtscript.IJK, np.float64]
+
+
+def lowdim_inputs(field_3d: F3D, field_2d: F2D, field_1d: F1DK):
+    with computation(PARALLEL):
+        with interval(0, -1):
+            tmp = field_2d + field_1d[1]
+        with interval(-1, None):
+            tmp = field_2d + field_1d[0]
+    with computation(PARALLEL):
+        with interval(0, 1):
+            field_3d = tmp[1, 0, 0] + field_1d[1]
+        with interval(1, None):
+            field_3d[0, 0, 0] = tmp[-1, 0, 0]
+
+
+case(
+    "lowdim_inputs",
+    fields={"field_3d": fs(6, 6, 6, init="zeros"), "field_2d": fs(6, 6), "field_1d": fs(6)},
+    origin=(1, 1, 0),
+    domain=(4, 3, 6),
+)(lowdim_inputs)
+
+
+def lowdim_masked(cond: F3D, inp: F2D, outp: F3D):
+    with computation(PARALLEL), interval(...):
+        if cond > 0.0:
+            outp[0, 0, 0] = inp
+
+
+case("lowdim_masked", fields={"cond": fs(10, 10, 10), "inp": fs(10, 10), "outp": fs(10, 10, 10)})(lowdim_masked)
+
+
+def lowdim_masked_forward(cond: F3D, inp: F2D, outp: F3D):
+    with computation(FORWARD), interval(...):
+        if cond > 0.0:
+            outp[0, 0, 0] = inp
+
+
+case(
+    "lowdim_masked_forward", fields={"cond": fs(10, 10, 10), "inp": fs(10, 10), "outp": fs(10, 10, 10)}
+)(lowdim_masked_forward)
+
+
+def k_only_access(in_field: F1DK, out_field: F64):
+    with computation(PARALLEL):
+        with interval(0, 1):
+            out_field[0, 0, 0] = in_field[1]
+        with interval(1, None):
+            out_field[0, 0, 0] = in_field[-1]
+
+
+case("k_only_access", fields={"in_field": fs(5), "out_field": fs(4, 4, 5, init="zeros")})(k_only_access)
+
+
+def lowdim_2d_output(a: F64, colsum: F2D):
+    with computation(FORWARD):
+        with interval(0, 1):
+            colsum = a
+        with interval(1, None):
+            colsum = colsum + a
+
+
+case("lowdim_2d_output", fields={"a": fs(7, 6, 5), "colsum": fs(7, 6, init="zeros")})(lowdim_2d_output)
+
+
+# --------------------------------------------------------------------------------------
+# Data dimensions, variable / written K offsets, global tables
+# (test_code_generation.py:309-361, 387-427, 463-510, 664-716, 815-1094, 1137-1222, 1604-1619)
+# --------------------------------------------------------------------------------------
+
+V2 = (np.float64, (2,))
+M22 = (np.float64, (2, 2))
+I32V2 = (np.int32, (2,))
+V4 = (np.float64, (4,))
+
+
+def higher_dimensional_fields(field: F64, vec_field: Field[V2], mat_field: Field[M22]):
+    with computation(PARALLEL), interval(...):
+        tmp = vec_field[0, 0, 0][0] + vec_field[0, 0, 0][1]  # noqa: F841
+    with computation(FORWARD):
+        with interval(0, 1):
+            vec_field[0, 0, 0][0] = field[1, 0, 0]
+            vec_field[0, 0, 0][1] = field[0, 1, 0]
+        with interval(1, -1):
+            vec_field[0, 0, 0][0] = 2 * field[1, 0, -1]
+            vec_field[0, 0, 0][1] = 2 * field[0, 1, -1]
+        with interval(-1, None):
+            vec_field[0, 0, 0][0] = field[1, 0, 0]
+            vec_field[0, 0, 0][1] = field[0, 1, 0]
+    with computation(PARALLEL), interval(...):
+        mat_field[0, 0, 0][0, 0] = vec_field[0, 0, 0][0] + 1.0
+        mat_field[0, 0, 0][1, 1] = vec_field[0, 0, 0][1] + 1.0
+
+
+case(
+    "higher_dimensional_fields",
+    fields={"field": fs(6, 6, 6), "vec_field": fs(6, 6, 6, 2), "mat_field": fs(6, 6, 6, 2, 2)},
+    origin=(1, 1, 0),
+    domain=(4, 4, 6),
+)(higher_dimensional_fields)
+
+
+def data_dim_stencil(vec_field: Field[V4], out_field: F64, *, idx: int):
+    with computation(PARALLEL), interval(...):
+        out_field[0, 0, 0] = vec_field[0, 0, 0][2] * vec_field[1, 0, 0][idx] - vec_field[0, -1, 0][3]
+
+
+case(
+    "data_dim_stencil",
+    fields={"vec_field": fs(8, 7, 5, 4), "out_field": fs(8, 7, 5, init="zeros")},
+    params={"idx": 1},
+    origin={"vec_field": (0, 1, 0, 0), "out_field": (0, 1, 0)},
+    domain=(7, 6, 5),
+)(data_dim_stencil)
+
+
+def data_dim_write_index(input_field: Field[gtscript.IJK, np.int32], output_field: Field[gtscript.IJK, I32V2], *, index: int):
+    with computation(PARALLEL), interval(...):
+        output_field[0, 0, 0][index] = input_field
+
+
+case(
+    "data_dim_write_index",
+    fields={"input_field": fs(3, 2, 4, dtype="i4", init=("int", -50, 50)),
+            "output_field": fs(3, 2, 4, 2, dtype="i4", init=("int", -5, 5))},
+    params={"index": 1},
+)(data_dim_write_index)
+
+
+def data_dim_read_index(input_field: Field[gtscript.IJK, I32V2], output_field: Field[gtscript.IJK, np.int32], *, index: int):
+    with computation(PARALLEL), interval(...):
+        output_field[0, 0, 0] = input_field[0, 0, 0][index]
+
+
+case(
+    "data_dim_read_index",
+    fields={"input_field": fs(3, 2, 4, 2, dtype="i4", init=("int", -50, 50)),
+            "output_field": fs(3, 2, 4, dtype="i4", init="zeros")},
+    params={"index": 1},
+)(data_dim_read_index)
+
+
+def variable_offsets_ij(in_field: F64, out_field: F64, index_field: Field[gtscript.IJ, np.int64]):
+    with computation(FORWARD), interval(...):
+        out_field[0, 0, 0] = in_field[0, 0, 1] + in_field[0, 0, index_field + 1]
+        index_field = index_field + 1
+
+
+case(
+    "variable_offsets_ij",
+    fields={"in_field": fs(5, 4, 12), "out_field": fs(5, 4, 12, init="zeros"),
+            "index_field": fs(5, 4, dtype="i8", init=("const", -3))},
+    domain=(5, 4, 6),
+)(variable_offsets_ij)
+
+
+def variable_offsets_ijk(in_field: F64, out_field: F64, index_field: Field[np.int64]):
+    with computation(PARALLEL), interval(...):
+        out_field[0, 0, 0] = in_field[0, 0, 1] + in_field[0, 0, index_field + 1]
+
+
+case(
+    "variable_offsets_ijk",
+    fields={"in_field": fs(5, 4, 10), "out_field": fs(5, 4, 10, init="zeros"),
+            "index_field": fs(5, 4, 10, dtype="i8", init=("int", -2, 3))},
+    origin=(0, 0, 2),
+    domain=(5, 4, 5),
+)(variable_offsets_ijk)
+
+
+def variable_offsets_and_while_loop(pe1: F64, pe2: F64, qin: F64, qout: F64, lev: Field[gtscript.IJ, np.int64]):
+    with computation(FORWARD), interval(0, -1):
+        if pe2[0, 0, 1] <= pe1[0, 0, lev]:
+            qout = qin[0, 0, 1]
+        else:
+            qsum = pe1[0, 0, lev + 1] - pe2[0, 0, lev]
+            while pe1[0, 0, lev + 1] < pe2[0, 0, 1]:
+                qsum += qin[0, 0, lev] / (pe2[0, 0, 1] - pe1[0, 0, lev])
+                lev = lev + 1
+            qout[0, 0, 0] = qsum / (pe2[0, 0, 1] - pe2)
+
+
+case(
+    "variable_offsets_and_while_loop",
+    fields={"pe1": fs(4, 3, 8, init=("ramp", 0.0, 1.0)), "pe2": fs(4, 3, 8, init=("ramp", 0.05, 0.9)),
+            "qin": fs(4, 3, 8), "qout": fs(4, 3, 8, init="zeros"),
+            "lev": fs(4, 3, dtype="i8", init=("const", 0))},
+)(variable_offsets_and_while_loop)
+
+
+def k_offset_scalar(in_field: F64, out_field: F64, scalar_value: int):
+    with computation(PARALLEL), interval(1, None):
+        out_field[0, 0, 0] = in_field[0, 0, scalar_value]
+
+
+case(
+    "k_offset_scalar",
+    fields={"in_field": fs(4, 4, 4), "out_field": fs(4, 4, 4, init="zeros")},
+    params={"scalar_value": -1},
+)(k_offset_scalar)
+
+
+def k_offset_field(in_field: F64, out_field: F64, idx_field: Field[gtscript.IJ, np.int64]):
+    with computation(PARALLEL), interval(1, None):
+        out_field[0, 0, 0] = in_field[0, 0, idx_field + 1]
+
+
+case(
+    "k_offset_field",
+    fields={"in_field": fs(4, 4, 4), "out_field": fs(4, 4, 4, init="zeros"),
+            "idx_field": fs(4, 4, dtype="i8", init=("int", -2, 1))},
+)(k_offset_field)
+
+
+def k_offset_write_simple(A: F64, B: F64):
+    with computation(FORWARD), interval(...):
+        B[0, 0, 1] = A
+
+
+case("k_offset_write_simple", fields={"A": fs(3, 2, 4), "B": fs(3, 2, 4, init="zeros")}, domain=(3, 2, 3))(
+    k_offset_write_simple
+)
+
+
+def k_offset_write_forward(A: F64, B: F64, scalar: np.float64):
+    with computation(FORWARD), interval(1, None):
+        A[0, 0, -1] = scalar
+        B[0, 0, 0] = A
+
+
+case("k_offset_write_forward", fields={"A": fs(3, 2, 5), "B": fs(3, 2, 5, init="zeros")}, params={"scalar": 2.0})(
+    k_offset_write_forward
+)
+
+
+def k_offset_write_backward(A: F64, B: F64, scalar: np.float64):
+    with computation(BACKWARD), interval(-1, None):
+        A = scalar
+    with computation(BACKWARD), interval(1, None):
+        A[0, 0, -1] = scalar
+        B[0, 0, 0] = A
+
+
+case("k_offset_write_backward", fields={"A": fs(3, 2, 5), "B": fs(3, 2, 5, init="zeros")}, params={"scalar": 2.0})(
+    k_offset_write_backward
+)
+
+
+def k_offset_write_conditional(A: F64, B: F64, scalar: np.float64):
+    with computation(BACKWARD), interval(1, -1):
+        if A > 0 and B > 0:
+            A[0, 0, -1] = scalar
+            B[0, 0, 1] = A
+        lev = 1
+        while A >= 0 and B >= 0:
+            A[0, 0, lev] = -1
+            B = -1
+            lev = lev + 1
+
+
+case(
+    "k_offset_write_conditional",
+    fields={"A": fs(3, 2, 4, init=("ramp", 40.0, 44.0)), "B": fs(3, 2, 4, init=("const", 1.0))},
+    params={"scalar": 2.0},
+)(k_offset_write_conditional)
+
+
+def cast_in_index(in_field: F64, i32: np.int32, i64: np.int64, out_field: F64):
+    with computation(PARALLEL), interval(...):
+        out_field[0, 0, 0] = in_field[0, 0, i32 - i64]
+
+
+case(
+    "cast_in_index",
+    fields={"in_field": fs(4, 3, 8), "out_field": fs(4, 3, 8, init="zeros")},
+    params={"i32": np.int32(3), "i64": np.int64(1)},
+    domain=(4, 3, 6),
+)(cast_in_index)
+
+
+def upcasting_k_index_write(in_field: F64, index_field: Field[gtscript.IJ, np.int32], out_field: F64):
+    with computation(FORWARD), interval(...):
+        out_field[0, 0, index_field - 1] = in_field
+
+
+case(
+    "upcasting_k_index_write",
+    fields={"in_field": fs(5, 5, 5), "index_field": fs(5, 5, dtype="i4", init=("const", 1)),
+            "out_field": fs(5, 5, 5, init="zeros")},
+)(upcasting_k_index_write)
+
+
+def lagrangian_contributions(q: F64, pe1: F64, pe2: F64, q4_1: F64, q4_2: F64, q4_3: F64, q4_4: F64, dp1: F64,
+                             lev: Field[gtscript.IJ, np.int64]):
+    with computation(FORWARD), interval(...):
+        pl = (pe2 - pe1[0, 0, lev]) / dp1[0, 0, lev]
+        if pe2[0, 0, 1] <= pe1[0, 0, lev + 1]:
+            pr = (pe2[0, 0, 1] - pe1[0, 0, lev]) / dp1[0, 0, lev]
+            q[0, 0, 0] = (
+                q4_2[0, 0, lev]
+                + 0.5 * (q4_4[0, 0, lev] + q4_3[0, 0, lev] - q4_2[0, 0, lev]) * (pr + pl)
+                - q4_4[0, 0, lev] * 1.0 / 3.0 * (pr * (pr + pl) + pl * pl)
+            )
+        else:
+            qsum = (pe1[0, 0, lev + 1] - pe2) * (
+                q4_2[0, 0, lev]
+                + 0.5 * (q4_4[0, 0, lev] + q4_3[0, 0, lev] - q4_2[0, 0, lev]) * (1.0 + pl)
+                - q4_4[0, 0, lev] * 1.0 / 3.0 * (1.0 + pl * (1.0 + pl))
+            )
+            lev = lev + 1
+            while pe1[0, 0, lev + 1] < pe2[0, 0, 1]:
+                qsum += dp1[0, 0, lev] * q4_1[0, 0, lev]
+                lev = lev + 1
+            dp = pe2[0, 0, 1] - pe1[0, 0, lev]
+            esl = dp / dp1[0, 0, lev]
+            qsum += dp * (
+                q4_2[0, 0, lev]
+                + 0.5 * esl * (q4_3[0, 0, lev] - q4_2[0, 0, lev] + q4_4[0, 0, lev] * (1.0 - (2.0 / 3.0) * esl))
+            )
+            q = qsum / (pe2[0, 0, 1] - pe2)
+        lev = lev - 1
+
+
+case(
+    "lagrangian_contributions",
+    fields={"q": fs(4, 3, 10, init="zeros"), "pe1": fs(4, 3, 10, init=("ramp", 0.0, 1.0)),
+            "pe2": fs(4, 3, 10, init=("ramp", 0.0, 0.95)), "q4_1": fs(4, 3, 10), "q4_2": fs(4, 3, 10),
+            "q4_3": fs(4, 3, 10), "q4_4": fs(4, 3, 10), "dp1": fs(4, 3, 10, init=("u", 0.5, 1.5)),
+            "lev": fs(4, 3, dtype="i8", init=("const", 0))},
+    domain=(4, 3, 8),
+)(lagrangian_contributions)
+
+
+def table_access(table_view: gtscript.GlobalTable[(np.float64, (4,))], out_field: F64):
+    with computation(PARALLEL):
+        with interval(0, 1):
+            out_field[0, 0, 0] = table_view.A[1]
+        with interval(1, None):
+            out_field[0, 0, 0] = table_view.A[2]
+
+
+case("table_access", fields={"table_view": fs(4), "out_field": fs(4, 4, 4, init="zeros")})(table_access)
+
+
+def direct_datadims_index(out: F64, inp: gtscript.GlobalTable[(np.float64, (2, 2, 2, 2))]):
+    with computation(PARALLEL), interval(...):
+        out[0, 0, 0] = inp.A[1, 0, 1, 0] + inp.A[0, 1, 1, 1]
+
+
+case("direct_datadims_index", fields={"out": fs(2, 2, 2, init="zeros"), "inp": fs(2, 2, 2, 2)})(
+    direct_datadims_index
+)

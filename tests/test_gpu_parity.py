@@ -43,8 +43,23 @@ def run_case_on_gpu(case):
     for k, v in host.items():
         if v is None:
             dev[k] = None
-        else:
+            continue
+        fi = stencil.field_info.get(k)
+        if fi is None:  # unused by the stencil: any layout
             dev[k] = storage.from_array(v, backend=BACKEND, aligned_index=_origin_of(case, k, v.ndim))
+            continue
+        axes = tuple(fi.axes)
+        dims = axes + tuple(str(d) for d in range(len(fi.data_dims)))
+        o = case.origin
+        if isinstance(o, dict):
+            org = tuple(o.get(k, o.get("_all_", (0,) * len(axes))))[: len(axes)]
+        elif o is None:
+            org = (0,) * len(axes)
+        else:
+            org = tuple(o["IJK".index(a)] for a in axes)
+        dev[k] = storage.from_array(
+            v, backend=BACKEND, aligned_index=org + (0,) * len(fi.data_dims), dimensions=dims
+        )
     kw = {}
     if case.origin is not None:
         kw["origin"] = case.origin
