@@ -28,6 +28,17 @@ from gt4py_amd.storage.layout import layout_checker_factory, layout_maker_factor
 _layout = layout_maker_factory((2, 1, 0))
 
 
+def generate_source(analysis, opts):
+    """(plan, HIP source, signature) of a typed stencil analysis: data-dimension lowering,
+    kernel planning, code generation."""
+    lowered, components = lower_data_dims(analysis)
+    plan = make_plan(lowered)
+    source, signature = hipgen.generate(
+        lowered, plan, opts, abi_fields=analysis.stencil.field_params(), components=components
+    )
+    return plan, source, signature
+
+
 class _Compiled:
     """The generated source, its library and the launcher that calls it."""
 
@@ -80,11 +91,7 @@ class Mi355xBackend(BaseBackend):
         b = self.builder
         opts = dict(b.options.backend_opts)
         t0 = time.perf_counter()
-        analysis, components = lower_data_dims(b.analysis)
-        plan = make_plan(analysis)
-        source, signature = hipgen.generate(
-            analysis, plan, opts, abi_fields=b.analysis.stencil.field_params(), components=components
-        )
+        plan, source, signature = generate_source(b.analysis, opts)
         t1 = time.perf_counter()
         path = jit.compile_source(source, verbose=bool(opts.get("verbose")))
         t2 = time.perf_counter()

@@ -140,7 +140,7 @@ class NumpyExecutor:
                     scalars[p.name] = p.dtype.np_dtype.type(v)
         for t in st.temporaries:
             (ilo, ihi), (jlo, jhi) = self.analysis.extents.fields.get(t.name, ((0, 0), (0, 0)))
-            arr = np.zeros((ni + ilo + ihi, nj + jlo + jhi, nk), dtype=t.dtype.np_dtype)
+            arr = np.zeros((ni + ilo + ihi, nj + jlo + jhi, nk) + tuple(t.data_dims), dtype=t.dtype.np_dtype)
             fields[t.name] = _Arr(arr, (ilo, jlo, 0), (True, True, True))
         self.fields, self.scalars, self.domain = fields, scalars, (ni, nj, nk)
         self.api = {p.name for p in st.field_params()}

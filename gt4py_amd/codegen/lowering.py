@@ -43,11 +43,19 @@ def _key(index: List[ir.Expr]) -> str:
 def lower_data_dims(analysis: StencilAnalysis) -> Tuple[StencilAnalysis, Dict[str, Component]]:
     st = analysis.stencil
     dd_fields = {p.name: p for p in st.field_params() if p.data_dims}
-    if not dd_fields:
+    dd_temps = {t.name: t for t in st.temporaries if t.data_dims}
+    if not dd_fields and not dd_temps:
         return analysis, {}
-    for t in st.temporaries:
-        if t.data_dims:
-            raise UnsupportedStencil(f"temporary '{t.name}' with data dimensions")
+    temp_comps: Dict[Tuple[str, Tuple[int, ...]], str] = {}
+
+    def temp_comp(acc: ir.FieldAccess) -> str:
+        if not all(isinstance(x, ir.Literal) for x in acc.data_index):
+            raise UnsupportedStencil(f"run-time data index into temporary '{acc.name}'")
+        idx = tuple(int(x.value) for x in acc.data_index)
+        k = (acc.name, idx)
+        if k not in temp_comps:
+            temp_comps[k] = f"{acc.name}__t{'_'.join(str(i) for i in idx)}"
+        return temp_comps[k]
 
     comps: Dict[str, Component] = {}
     by_key: Dict[Tuple[str, str], str] = {}
@@ -66,6 +74,8 @@ def lower_data_dims(analysis: StencilAnalysis) -> Tuple[StencilAnalysis, Dict[st
     def fn(e):
         if isinstance(e, ir.FieldAccess) and e.name in dd_fields:
             return ir.FieldAccess(comp_name(e), e.offset, e.dtype, [], e.k_offset)
+        if isinstance(e, ir.FieldAccess) and e.name in dd_temps:
+            return ir.FieldAccess(temp_comp(e), e.offset, e.dtype, [], e.k_offset)
         return e
 
     # a written field: its components must be provably distinct (literal indices) or just one
@@ -95,7 +105,9 @@ def lower_data_dims(analysis: StencilAnalysis) -> Tuple[StencilAnalysis, Dict[st
             continue
         params.append(p)
     params += virtual_decls
-    lowered = ir.Stencil(st.name, st.api_signature, params, st.temporaries, loops, st.externals, st.docstring)
+    temps = [t for t in st.temporaries if t.name not in dd_temps]
+    temps += [ir.FieldDecl(v, dd_temps[n].dtype, dd_temps[n].axes, (), True) for (n, _), v in temp_comps.items()]
+    lowered = ir.Stencil(st.name, st.api_signature, params, temps, loops, st.externals, st.docstring)
     extents = passes.compute_extents(lowered)
     out = StencilAnalysis(
         lowered,

@@ -439,6 +439,89 @@ class StencilParser:
                 res.append(ir.HorizontalInterval(b, ir.AxisBound(b.level, b.offset + 1)))
         return ir.HorizontalMask(res[0], res[1])
 
+    def _declare_temporary(self, stmt: ast.AnnAssign, scope: _Scope) -> List[ir.VerticalLoop]:
+        """Top-level ``tmp: Field[(dtype, (n, m))] = value``: an IJK temporary (optionally with data
+        dimensions) initialised by a full-domain PARALLEL computation
+        (reference ``gtscript_frontend.py:2183-2230``, ``_make_init_computations`` ``:791-830``)."""
+        from gt4py_amd.gtscript import IJK, _FieldDescriptor
+
+        desc = self._const_eval(stmt.annotation, scope)
+        if not isinstance(desc, _FieldDescriptor):
+            raise GTScriptSyntaxError("Top-level annotated assignments must declare Field temporaries")
+        if tuple(desc.axes_names) != tuple(a.name for a in IJK):
+            raise GTScriptSyntaxError(
+                f"Found {''.join(desc.axes_names)}, but only IJK is currently supported for temporaries"
+            )
+        name = stmt.target.id
+        dtype = DataType.from_np(desc.dtype)
+        tname = self._temp_for_local(name, scope, create=True)
+        self.temporaries[tname] = ir.FieldDecl(tname, dtype, ("I", "J", "K"), tuple(desc.data_dims), is_temporary=True)
+        self.temp_declared_dtype[tname] = dtype
+        if stmt.value is None:
+            return []
+        value = self._const_eval(stmt.value, scope)
+        body = []
+        for index in itertools.product(*(range(n) for n in desc.data_dims)):
+            didx = [ir.Literal(i, DataType.INT32) for i in index]
+            body.append(ir.Assign(ir.FieldAccess(tname, (0, 0, 0), data_index=didx), ir.Literal(value, dtype)))
+        full = ir.Interval(ir.AxisBound(ir.LevelMarker.START, 0), ir.AxisBound(ir.LevelMarker.END, 0))
+        return [ir.VerticalLoop(ir.LoopOrder.PARALLEL, [ir.Section(full, body)])]
+
+    # ------------------------------------------------------------------ vector expressions
+    def _vector_expr(self, node, scope: _Scope, pre):
+        """Nested lists of component expressions for a data-dimension expression, or a scalar
+        ``ir.Expr`` (reference ``defir_to_gtir.py:123-291``: UnrollVectorAssignments/Expressions)."""
+        if isinstance(node, (ast.Name, ast.Subscript)):
+            base = node
+            offs = (0, 0, 0)
+            if isinstance(node, ast.Subscript):
+                base = node.value
+            if isinstance(base, ast.Name):
+                decl = self._decl_of(base.id, scope)
+                if decl is not None and decl.data_dims:
+                    if isinstance(node, ast.Subscript):
+                        offs = self._parse_offset(node.slice, scope, pre)
+                    dims = decl.data_dims
+                    if len(dims) > 2:
+                        raise GTScriptSyntaxError("Higher dimensional fields only supported for vectors and matrices.")
+
+                    def comp(idx):
+                        didx = [ir.Literal(i, DataType.INT32) for i in idx]
+                        return self._resolve_name(base.id, scope, offs, didx)
+
+                    if len(dims) == 1:
+                        return [comp((a,)) for a in range(dims[0])]
+                    return [[comp((a, b)) for b in range(dims[1])] for a in range(dims[0])]
+        if isinstance(node, ast.Attribute) and node.attr == "T":
+            m = self._vector_expr(node.value, scope, pre)
+            if not (isinstance(m, list) and m and isinstance(m[0], list)):
+                raise GTScriptSyntaxError("'.T' needs a matrix")
+            return [list(r) for r in zip(*m)]
+        if isinstance(node, ast.UnaryOp) and isinstance(node.op, (ast.USub, ast.UAdd)):
+            v = self._vector_expr(node.operand, scope, pre)
+            if isinstance(v, list):
+                op = "-" if isinstance(node.op, ast.USub) else "+"
+                return _vmap(lambda x: ir.UnaryOp(op, x), v)
+        if isinstance(node, ast.BinOp):
+            lhs = self._vector_expr(node.left, scope, pre)
+            rhs = self._vector_expr(node.right, scope, pre)
+            if isinstance(node.op, ast.MatMult):
+                if not (isinstance(lhs, list) and isinstance(lhs[0], list) and isinstance(rhs, list)):
+                    raise GTScriptSyntaxError("'@' needs a matrix and a vector")
+                out = []
+                for row in lhs:
+                    acc = ir.BinaryOp("*", row[0], rhs[0])
+                    for a, b in zip(row[1:], rhs[1:]):
+                        acc = ir.BinaryOp("+", acc, ir.BinaryOp("*", a, b))
+                    out.append(acc)
+                return out
+            if isinstance(lhs, list) or isinstance(rhs, list):
+                op = {ast.Add: "+", ast.Sub: "-", ast.Mult: "*", ast.Div: "/"}.get(type(node.op))
+                if op is None:
+                    raise GTScriptSyntaxError(f"Unsupported vector operator {type(node.op).__name__}")
+                return _vzip(lambda a, b: ir.BinaryOp(op, a, b), lhs, rhs)
+        return self._parse_expr(node, scope, pre)
+
     def _temp_for_local(self, name: str, scope: _Scope, create: bool) -> Optional[str]:
         if name in scope.locals:
             return scope.locals[name]
@@ -460,6 +543,29 @@ class StencilParser:
             out = pre
             for t, r in zip(target.elts, results):
                 out.extend(self._assign_to(t, r, scope))
+            return out
+        tdecl = None
+        tbase = target.value if isinstance(target, ast.Subscript) else target
+        if isinstance(tbase, ast.Name):
+            tdecl = self._decl_of(tbase.id, scope)
+        if tdecl is not None and tdecl.data_dims:
+            # whole-field assignment to a data-dimension field: one assignment per component
+            vec = self._vector_expr(value, scope, pre)
+            out = pre
+            for index in itertools.product(*(range(n) for n in tdecl.data_dims)):
+                v = vec
+                for i in index:
+                    v = v[i] if isinstance(v, list) else v
+                if isinstance(v, list):
+                    raise GTScriptSyntaxError(f"Assignment dimension mismatch for '{tbase.id}'")
+                sub = ast.Subscript(
+                    value=target if isinstance(target, ast.Subscript) else ast.Subscript(
+                        value=tbase, slice=ast.Tuple(elts=[ast.Constant(0)] * 3, ctx=ast.Load()), ctx=ast.Store()
+                    ),
+                    slice=ast.Tuple(elts=[ast.Constant(i) for i in index], ctx=ast.Load()),
+                    ctx=ast.Store(),
+                )
+                out = out + self._assign_to(sub, v, scope)
             return out
         val = self._parse_expr(value, scope, pre)
         return pre + self._assign_to(target, val, scope)
@@ -871,6 +977,8 @@ class StencilParser:
                 self._parse_import(stmt, scope)
             elif isinstance(stmt, ast.With):
                 loops.extend(self._parse_computation(stmt, scope))
+            elif isinstance(stmt, ast.AnnAssign) and isinstance(stmt.target, ast.Name):
+                loops.extend(self._declare_temporary(stmt, scope))
             elif isinstance(stmt, ast.Pass) or (
                 isinstance(stmt, ast.Expr) and isinstance(getattr(stmt, "value", None), ast.Constant)
             ):
@@ -890,6 +998,22 @@ class StencilParser:
             externals=dict(self.used_externals),
             docstring=inspect.getdoc(func) or "",
         )
+
+
+def _vmap(fn, v):
+    return [_vmap(fn, x) for x in v] if isinstance(v, list) else fn(v)
+
+
+def _vzip(fn, a, b):
+    if isinstance(a, list) and isinstance(b, list):
+        if len(a) != len(b):
+            raise GTScriptSyntaxError("Vector operands of different lengths")
+        return [_vzip(fn, x, y) for x, y in zip(a, b)]
+    if isinstance(a, list):
+        return [_vzip(fn, x, b) for x in a]
+    if isinstance(b, list):
+        return [_vzip(fn, a, y) for y in b]
+    return fn(a, b)
 
 
 def _load_copy(target):

@@ -64,11 +64,12 @@ def _expr(node) -> ir.Expr:
         return _literal(node)
     if isinstance(node, gtir.FieldAccess):
         off = node.offset
+        didx = [_expr(x) for x in (node.data_index or [])]
+        if isinstance(off, gtir.VariableKOffset):
+            return ir.FieldAccess(node.name, (0, 0, 0), _dt(node.dtype), didx, _expr(off.k))
         if not hasattr(off, "i"):
-            raise NotImplementedError("variable K offsets are not supported by gt:mi355x")
-        if node.data_index:
-            raise NotImplementedError("data dimensions are not supported by gt:mi355x")
-        return ir.FieldAccess(node.name, (int(off.i), int(off.j), int(off.k)), _dt(node.dtype))
+            raise NotImplementedError("absolute K indexing is not supported by gt:mi355x")
+        return ir.FieldAccess(node.name, (int(off.i), int(off.j), int(off.k)), _dt(node.dtype), didx)
     if isinstance(node, gtir.ScalarAccess):
         return ir.ScalarAccess(node.name, _dt(node.dtype))
     if isinstance(node, gtir.IteratorAccess):
@@ -247,9 +248,7 @@ def register():
     from gt4py.storage.cartesian import layout as gt_layout
 
     from gt4py_amd import passes
-    from gt4py_amd.backend.mi355x_backend import Mi355xBackend
-    from gt4py_amd.codegen import hip as hipgen
-    from gt4py_amd.codegen.plan import make_plan
+    from gt4py_amd.backend.mi355x_backend import Mi355xBackend, generate_source
     from gt4py_amd.runtime import jit
 
     GTMIStencilObject = _stencil_object_base()
@@ -295,8 +294,7 @@ def register():
             opts = dict(self.builder.options.backend_opts)
             stencil_ir = gtir_to_ir(self.builder.gtir_pipeline.full())
             analysis = passes.run_pipeline(stencil_ir)
-            plan = make_plan(analysis)
-            source, _ = hipgen.generate(analysis, plan, opts)
+            _, source, _ = generate_source(analysis, opts)
             return jit.compile_source(source, verbose=bool(opts.get("verbose")))
 
         def generate(self):

@@ -19,8 +19,10 @@ sys.modules["gt4py_amd.gtscript"] = real_mod; gt4py_amd.gtscript = real_mod
 from gt4py_amd import gt4py_plugin
 gt4py_plugin.register()
 from gt4py_amd import gtscript as my
-names = sys.argv[1:] or ["hdiff_f64", "hdiff_f32", "tridiag", "lap5", "copy", "vertical_advection_dycore", "suite_hdiff_weight", "native_functions", "horizontal_regions", "suite_runtime_if_nested_while"]
-STRICT = {"hdiff_f64", "hdiff_f32", "tridiag", "lap5", "copy", "vertical_advection_dycore", "suite_hdiff_weight"}
+names = sys.argv[1:] or ["hdiff_f64", "hdiff_f32", "tridiag", "lap5", "copy", "vertical_advection_dycore", "suite_hdiff_weight", "native_functions", "horizontal_regions", "suite_runtime_if_nested_while", "higher_dimensional_fields", "variable_offsets_ij", "k_offset_write_backward", "lowdim_inputs", "suite_matmul", "suite_typed_temporary", "data_dim_stencil"]
+STRICT = {"hdiff_f64", "hdiff_f32", "tridiag", "lap5", "copy", "vertical_advection_dycore", "suite_hdiff_weight",
+          "higher_dimensional_fields", "variable_offsets_ij", "k_offset_write_backward", "lowdim_inputs", "suite_matmul",
+          "suite_typed_temporary", "data_dim_stencil"}
 bad = []
 for name in names:
     case = sc_ref.CASES[name]

@@ -1560,3 +1560,281 @@ def direct_datadims_index(out: F64, inp: gtscript.GlobalTable[(np.float64, (2, 2
 case("direct_datadims_index", fields={"out": fs(2, 2, 2, init="zeros"), "inp": fs(2, 2, 2, 2)})(
     direct_datadims_index
 )
+
+
+# --------------------------------------------------------------------------------------
+# Remaining StencilTestSuite definitions (test_suites.py:614-1160): lower-dimensional and
+# data-dimension fields, reads outside the K interval, variable K reads, regions, typed and
+# vector temporaries, vector/matrix expressions
+# --------------------------------------------------------------------------------------
+
+
+def suite_non3d_fields(
+    field_in: Field[gtscript.K, np.float64],
+    another_field: Field[gtscript.IJ, (np.float64, (3, 2, 2))],
+    field_out: Field[gtscript.IJK, (np.float64, (3, 2))],
+):
+    with computation(PARALLEL), interval(...):
+        field_out[0, 0, 0][0, 0] = field_in[0] + another_field[-1, -1][0, 0, 0] + another_field[-1, -1][0, 0, 1]
+        field_out[0, 0, 0][0, 1] = 2 * (
+            another_field[-1, -1][1, 0, 0]
+            + another_field[-1, -1][1, 0, 1]
+            + another_field[-1, -1][1, 1, 0]
+            + another_field[-1, -1][1, 1, 1]
+        )
+        field_out[0, 0, 0][1, 0] = field_in[0] + another_field[1, 1][0, 0, 0] + another_field[1, 1][0, 0, 1]
+        field_out[0, 0, 0][1, 1] = 3 * (
+            another_field[1, 1][1, 0, 0]
+            + another_field[1, 1][1, 0, 1]
+            + another_field[1, 1][1, 1, 0]
+            + another_field[1, 1][1, 1, 1]
+        )
+        field_out[0, 0, 0][2, 0] = field_in[0] + another_field[0, 0][0, 0, 0] + another_field[-1, 1][0, 0, 1]
+        field_out[0, 0, 0][2, 1] = 4 * (
+            another_field[-1, 1][1, 0, 0]
+            + another_field[-1, 1][1, 0, 1]
+            + another_field[-1, 1][1, 1, 0]
+            + another_field[-1, 1][1, 1, 1]
+        )
+
+
+case(
+    "suite_non3d_fields",
+    fields={"field_in": fs(6), "another_field": fs(9, 7, 3, 2, 2), "field_out": fs(7, 5, 6, 3, 2)},
+    origin={"field_in": (0,), "another_field": (1, 1), "field_out": (0, 0, 0)},
+    domain=(7, 5, 6),
+)(suite_non3d_fields)
+
+
+def suite_read_outside_k1(field_in: F64, field_out: F64):
+    with computation(PARALLEL), interval(...):
+        field_out = field_in[0, 0, -1] + field_in[0, 0, 1]
+
+
+case(
+    "suite_read_outside_k1",
+    fields={"field_in": fs(4, 4, 6), "field_out": fs(4, 4, 4)},
+    origin={"field_in": (0, 0, 1), "field_out": (0, 0, 0)},
+    domain=(4, 4, 4),
+)(suite_read_outside_k1)
+
+
+def suite_read_outside_k2(field_in: F64, field_out: F64):
+    with computation(PARALLEL), interval(-1, None):
+        field_out = field_in[0, 0, 1]
+
+
+case(
+    "suite_read_outside_k2",
+    fields={"field_in": fs(4, 4, 5), "field_out": fs(4, 4, 4)},
+    domain=(4, 4, 4),
+)(suite_read_outside_k2)
+
+
+def suite_read_outside_k3(field_in: F64, field_out: F64):
+    with computation(PARALLEL), interval(0, 1):
+        field_out = field_in[0, 0, -1]
+
+
+case(
+    "suite_read_outside_k3",
+    fields={"field_in": fs(4, 4, 5), "field_out": fs(4, 4, 4)},
+    origin={"field_in": (0, 0, 1), "field_out": (0, 0, 0)},
+    domain=(4, 4, 4),
+)(suite_read_outside_k3)
+
+
+def suite_variable_k_read(
+    field_in: Field[np.float32], field_out: Field[np.float32], index: Field[gtscript.K, np.int32]
+):
+    with computation(PARALLEL), interval(1, None):
+        field_out = field_in[0, 0, index]
+
+
+case(
+    "suite_variable_k_read",
+    fields={"field_in": fs(2, 2, 8, dtype="f4"), "field_out": fs(2, 2, 8, dtype="f4"),
+            "index": fs(8, dtype="i4", init=("int", -1, 1))},
+)(suite_variable_k_read)
+
+
+def suite_variable_k_and_read_outside(field_in: F64, field_out: F64, index: Field[gtscript.K, np.int32]):
+    with computation(PARALLEL), interval(1, None):
+        field_out[0, 0, 0] = field_in[0, 0, index] + field_in[0, 0, -2]
+
+
+case(
+    "suite_variable_k_and_read_outside",
+    fields={"field_in": fs(2, 2, 9, init=("u", 0.1, 10.0)), "field_out": fs(2, 2, 8, init=("u", 0.1, 10.0)),
+            "index": fs(8, dtype="i4", init=("int", -1, 1))},
+    origin={"field_in": (0, 0, 1), "field_out": (0, 0, 0), "index": (0,)},
+    domain=(2, 2, 8),
+)(suite_variable_k_and_read_outside)
+
+
+def suite_diagonal_k_offset(field_in: F64, field_out: F64):
+    with computation(PARALLEL), interval(...):
+        field_out = field_in[0, 0, 1]
+    with computation(PARALLEL), interval(0, -1):
+        field_out += field_in[0, -1, 1]
+
+
+case(
+    "suite_diagonal_k_offset",
+    fields={"field_in": fs(2, 3, 9, init=("u", 0.1, 10.0)), "field_out": fs(2, 2, 8)},
+    origin={"field_in": (0, 1, 0), "field_out": (0, 0, 0)},
+    domain=(2, 2, 8),
+)(suite_diagonal_k_offset)
+
+
+def suite_horizontal_regions(field_in: Field[np.float32], field_out: Field[np.float32]):
+    with computation(PARALLEL), interval(...):
+        field_out = field_in
+        with horizontal(region[I[0], :], region[I[-1], :]):
+            field_out = field_in + 1.0
+        with horizontal(region[:, J[0]], region[:, J[-1]]):
+            field_out = field_in - 1.0
+
+
+case("suite_horizontal_regions", fields={"field_in": fs(4, 4, 2, dtype="f4"), "field_out": fs(4, 4, 2, dtype="f4")})(
+    suite_horizontal_regions
+)
+
+
+def suite_horizontal_regions_partial(field_in: Field[np.float32], field_out: Field[np.float32]):
+    with computation(PARALLEL), interval(...):
+        with horizontal(region[I[0], :], region[I[-1], :]):
+            field_out = field_in + 1.0
+        with horizontal(region[:, J[0]], region[:, J[-1]]):
+            field_out = field_in - 1.0
+
+
+case(
+    "suite_horizontal_regions_partial",
+    fields={"field_in": fs(4, 4, 2, dtype="f4"), "field_out": fs(4, 4, 2, dtype="f4", init=("const", 42.0))},
+)(suite_horizontal_regions_partial)
+
+
+def suite_horizontal_regions_corners(field_in: Field[np.float32], field_out: Field[np.float32]):
+    with computation(PARALLEL), interval(...):
+        with horizontal(region[I[0] : I[0] + 2, J[0] : J[0] + 2], region[I[-1] - 2 : I[-1], J[-1] - 2 : J[-1]]):
+            field_out = field_in + 1.0
+        with horizontal(region[I[0] : I[0] + 2, J[-1] - 2 : J[-1]], region[I[-1] - 2 : I[-1], J[0] : J[0] + 2]):
+            field_out = field_in - 1.0
+
+
+case(
+    "suite_horizontal_regions_corners",
+    fields={"field_in": fs(6, 5, 2, dtype="f4"), "field_out": fs(6, 5, 2, dtype="f4", init=("const", 42.0))},
+)(suite_horizontal_regions_corners)
+
+
+def suite_typed_temporary(field_in: Field[np.float32], field_out: Field[np.float32]):
+    tmp: Field[(np.float32, (2, 2))] = 0
+    with computation(PARALLEL):
+        with interval(0, -1):
+            tmp[0, 0, 0][0, 0] = field_in[0, 0, 0]
+            tmp[0, 0, 0][1, 0] = field_in[0, 0, 1]
+            tmp[0, 0, 0][0, 1] = -1.0
+            tmp[0, 0, 0][1, 1] = -1.0
+            field_out = tmp[0, 0, 0][0, 0] + tmp[0, 0, 0][1, 0]
+        with interval(-1, None):
+            field_out = 0
+
+
+case(
+    "suite_typed_temporary", fields={"field_in": fs(2, 2, 8, dtype="f4"), "field_out": fs(2, 2, 8, dtype="f4")}
+)(suite_typed_temporary)
+
+
+F64V2 = Field[(np.float64, (2,))]
+F32V2 = Field[(np.float32, (2,))]
+
+
+def suite_vector_gen_assignment(field_in: F64V2, field_out: F64V2):
+    with computation(PARALLEL), interval(...):
+        field_out = 2 * field_in
+
+
+case("suite_vector_gen_assignment", fields={"field_in": fs(3, 2, 2, 2), "field_out": fs(3, 2, 2, 2)})(
+    suite_vector_gen_assignment
+)
+
+
+def suite_matrix_assignment(field_in: Field[(np.float32, (2, 3))], field_out: Field[(np.float32, (2, 3))]):
+    with computation(PARALLEL), interval(...):
+        field_out = field_in
+
+
+case(
+    "suite_matrix_assignment",
+    fields={"field_in": fs(2, 2, 2, 2, 3, dtype="f4"), "field_out": fs(2, 2, 2, 2, 3, dtype="f4")},
+)(suite_matrix_assignment)
+
+
+def suite_vector_vector_op(field_1: F32V2, field_2: F32V2, field_out: F32V2):
+    with computation(PARALLEL), interval(...):
+        field_out = field_1 + field_2
+
+
+case(
+    "suite_vector_vector_op",
+    fields={"field_1": fs(2, 2, 2, 2, dtype="f4"), "field_2": fs(2, 2, 2, 2, dtype="f4"),
+            "field_out": fs(2, 2, 2, 2, dtype="f4")},
+)(suite_vector_vector_op)
+
+
+def suite_combined_vector_scalar_op(field_1: F64V2, field_2: F64V2, field_out: F64V2):
+    with computation(PARALLEL), interval(...):
+        field_out = 3 * (field_1 + field_2 * field_2)
+
+
+case(
+    "suite_combined_vector_scalar_op",
+    fields={"field_1": fs(2, 2, 2, 2, init=("u", 1.0, 10.0)), "field_2": fs(2, 2, 2, 2, init=("u", 1.0, 10.0)),
+            "field_out": fs(2, 2, 2, 2)},
+)(suite_combined_vector_scalar_op)
+
+
+def suite_vectorized_temporary(field_in: F32V2, field_out: F32V2):
+    tmp: Field[(np.float32, (2,))] = 0
+    with computation(PARALLEL), interval(...):
+        tmp[0, 0, 0][0] = 2
+        tmp[0, 0, 0][1] = 3
+        field_out = tmp * field_in
+
+
+case(
+    "suite_vectorized_temporary",
+    fields={"field_in": fs(2, 2, 2, 2, dtype="f4"), "field_out": fs(2, 2, 2, 2, dtype="f4")},
+)(suite_vectorized_temporary)
+
+
+def suite_matmul(matrix: Field[(np.float64, (4, 6))], field_1: Field[(np.float64, (6,))],
+                 field_2: Field[(np.float64, (4,))]):
+    with computation(PARALLEL):
+        with interval(0, 1):
+            field_2 = matrix @ field_1
+        with interval(1, 2):
+            field_1 = matrix.T @ field_2
+
+
+case(
+    "suite_matmul",
+    fields={"matrix": fs(2, 2, 2, 4, 6), "field_1": fs(2, 2, 2, 6), "field_2": fs(2, 2, 2, 4)},
+)(suite_matmul)
+
+
+def suite_masked_matmul(matrix: Field[gtscript.K, (np.float64, (4, 6))], field_1: Field[(np.float64, (6,))],
+                        field_2: Field[(np.float64, (4,))]):
+    with computation(PARALLEL):
+        with interval(0, 1):
+            field_2 = matrix @ field_1
+        with interval(1, 2):
+            field_1 = matrix.T @ field_2
+
+
+case(
+    "suite_masked_matmul",
+    fields={"matrix": fs(2, 4, 6), "field_1": fs(2, 2, 2, 6), "field_2": fs(2, 2, 2, 4)},
+)(suite_masked_matmul)
