@@ -19,8 +19,8 @@ import time
 
 from gt4py_amd.backend.base import BaseBackend, register
 from gt4py_amd.codegen import hip as hipgen
-from gt4py_amd.codegen.lowering import lower_data_dims
-from gt4py_amd.codegen.plan import make_plan
+from gt4py_amd.codegen.lowering import lower_data_dims, split_phases
+from gt4py_amd.codegen.plan import UnsupportedStencil, make_plan
 from gt4py_amd.runtime import jit
 from gt4py_amd.runtime.launcher import StencilLauncher
 from gt4py_amd.storage.layout import layout_checker_factory, layout_maker_factory
@@ -32,10 +32,18 @@ def generate_source(analysis, opts):
     """(plan, HIP source, signature) of a typed stencil analysis: data-dimension lowering,
     kernel planning, code generation."""
     lowered, components = lower_data_dims(analysis)
-    plan = make_plan(lowered)
-    source, signature = hipgen.generate(
-        lowered, plan, opts, abi_fields=analysis.stencil.field_params(), components=components
-    )
+    abi = analysis.stencil.field_params()
+    try:
+        plan = make_plan(lowered)
+        source, signature = hipgen.generate(lowered, plan, opts, abi_fields=abi, components=components)
+    except UnsupportedStencil as direct_failure:
+        # staged fallback: split computations into phases, column kernels + scratch temporaries
+        try:
+            staged = split_phases(lowered)
+            plan = make_plan(staged, column_only=True)
+            source, signature = hipgen.generate(staged, plan, opts, abi_fields=abi, components=components)
+        except UnsupportedStencil as staged_failure:
+            raise UnsupportedStencil(f"{direct_failure}; staged lowering: {staged_failure}") from None
     return plan, source, signature
 
 

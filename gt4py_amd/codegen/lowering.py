@@ -117,3 +117,113 @@ def lower_data_dims(analysis: StencilAnalysis) -> Tuple[StencilAnalysis, Dict[st
         analysis.min_k_size,
     )
     return out, comps
+
+
+# ------------------------------------------------------------------------------------------
+# phase splitting: the general multi-stage lowering (column kernels + scratch temporaries)
+# ------------------------------------------------------------------------------------------
+
+
+def _stmt_accesses(s):
+    reads, writes = [], []
+    for acc, w in passes.iter_accesses([s]):
+        if isinstance(acc, ir.FieldAccess):
+            (writes if w else reads).append(acc)
+    return reads, writes
+
+
+def _loop_phases(vl: ir.VerticalLoop) -> List[int]:
+    """Phase of every top-level statement (flattened over sections, program order).
+
+    Splitting a computation into phases (one sub-computation per phase, same order and intervals)
+    is legal when every value a statement reads is still produced before (RAW) or after (WAR) the
+    read, as in the original order; an access at a horizontal offset (another column) or, inside one
+    column, at a vertical offset the sweep has not reached, needs the two statements in different
+    phases. Constraints ``phase(b) >= phase(a) + d`` are solved by longest paths; a positive cycle
+    means the computation cannot be staged.
+    """
+    stmts = [s for sec in vl.sections for s in sec.body]
+    n = len(stmts)
+    acc = [_stmt_accesses(s) for s in stmts]
+    fwd = vl.loop_order != ir.LoopOrder.BACKWARD
+    par = vl.loop_order == ir.LoopOrder.PARALLEL
+    edges = []  # (a, b, d): phase[b] >= phase[a] + d
+    for si in range(n):
+        for r in acc[si][0]:
+            for wi in range(n):
+                for w in acc[wi][1]:
+                    if w.name != r.name:
+                        continue
+                    di, dj, dk = r.offset
+                    dk -= w.offset[2]
+                    ij = bool(di or dj)
+                    var_k = r.k_offset is not None or w.k_offset is not None
+                    if par:
+                        raw = wi < si
+                        d = 1 if (ij or dk or var_k) else 0
+                    else:
+                        if var_k:
+                            # unknown level: keep reader and writer in one column sweep
+                            if ij:
+                                raise UnsupportedStencil(f"'{r.name}': run-time K offset across columns")
+                            if wi != si:
+                                edges.append((wi, si, 0))
+                                edges.append((si, wi, 0))
+                            continue
+                        before = dk < 0 if fwd else dk > 0
+                        raw = before or (dk == 0 and wi < si)
+                        d = 1 if ij else 0
+                    if wi == si:
+                        if raw and d:
+                            raise UnsupportedStencil(f"'{r.name}' feeds itself at a horizontal offset")
+                        continue
+                    edges.append((wi, si, d) if raw else (si, wi, d))
+    for a in range(n):  # writers of one name keep their order
+        for b in range(a + 1, n):
+            if {w.name for w in acc[a][1]} & {w.name for w in acc[b][1]}:
+                edges.append((a, b, 0))
+    phase = [0] * n
+    for _ in range(n + 1):
+        changed = False
+        for a, b, d in edges:
+            if phase[b] < phase[a] + d:
+                phase[b] = phase[a] + d
+                changed = True
+        if not changed:
+            return phase
+    raise UnsupportedStencil("statements depend on each other across columns in both directions")
+
+
+def split_phases(analysis: StencilAnalysis) -> StencilAnalysis:
+    """Split every computation into its phases (``_loop_phases``) so that each piece can run as
+    a column kernel; temporaries crossing pieces become scratch fields in the plan."""
+    st = analysis.stencil
+    loops: List[ir.VerticalLoop] = []
+    for vl in st.vertical_loops:
+        phases = _loop_phases(vl)
+        if not phases or max(phases) == 0:
+            loops.append(vl)
+            continue
+        for p in range(max(phases) + 1):
+            secs = []
+            t = 0
+            for sec in vl.sections:
+                body = []
+                for s in sec.body:
+                    if phases[t] == p:
+                        body.append(s)
+                    t += 1
+                if body:
+                    secs.append(ir.Section(sec.interval, body))
+            if secs:
+                loops.append(ir.VerticalLoop(vl.loop_order, secs))
+    if len(loops) == len(st.vertical_loops):
+        return analysis
+    new = dataclasses.replace(st, vertical_loops=loops)
+    return StencilAnalysis(
+        new,
+        passes.compute_access_kinds(new),
+        passes.compute_extents(new),
+        passes.compute_k_boundary(new),
+        analysis.min_k_size,
+    )

@@ -72,7 +72,10 @@ def _has_horizontal_offsets(vl: ir.VerticalLoop) -> bool:
     return False
 
 
-def make_plan(analysis: StencilAnalysis) -> KernelPlan:
+def make_plan(analysis: StencilAnalysis, column_only: bool = False) -> KernelPlan:
+    """``column_only``: every computation runs in column kernels (the staged fallback, after
+    ``lowering.split_phases``); otherwise PARALLEL computations with horizontal offsets become
+    J-streaming plane kernels."""
     st = analysis.stencil
     temps = {t.name for t in st.temporaries}
     api = {p.name for p in st.field_params()}
@@ -84,9 +87,11 @@ def make_plan(analysis: StencilAnalysis) -> KernelPlan:
         if run:
             kernels.append(ColumnKernel(list(run)))
             run.clear()
+        run_written.clear()
 
+    run_written: Set[str] = set()
     for li, vl in enumerate(st.vertical_loops):
-        if vl.loop_order == ir.LoopOrder.PARALLEL and _has_horizontal_offsets(vl):
+        if not column_only and vl.loop_order == ir.LoopOrder.PARALLEL and _has_horizontal_offsets(vl):
             if any(isinstance(a, ir.FieldAccess) and a.k_offset is not None for a, _ in _loop_accesses(vl)):
                 raise UnsupportedStencil("run-time K offsets in a PARALLEL computation with horizontal offsets")
             flush()
@@ -110,8 +115,15 @@ def make_plan(analysis: StencilAnalysis) -> KernelPlan:
                             f"'{acc.name}' is written in a {vl.loop_order.name} loop and read at a horizontal "
                             f"offset {acc.offset[:2]} in the same loop"
                         )
+            # a column kernel may not consume values at IJ offsets produced earlier in the same run
+            if any(
+                not w and isinstance(a, ir.FieldAccess) and a.name in run_written and (a.offset[0] or a.offset[1])
+                for a, w in _loop_accesses(vl)
+            ):
+                flush()
+                run_written.clear()
             run.append(li)
-            # a column kernel may not consume temporaries at IJ offsets produced in the same run
+            run_written.update(a.name for a, w in _loop_accesses(vl) if w)
     flush()
 
     # which kernel(s) / loops touch each temporary

@@ -1838,3 +1838,55 @@ case(
     "suite_masked_matmul",
     fields={"matrix": fs(2, 4, 6), "field_1": fs(2, 2, 2, 6), "field_2": fs(2, 2, 2, 4)},
 )(suite_masked_matmul)
+
+
+# --------------------------------------------------------------------------------------
+# Patterns the plane / single-column kernels cannot take directly: the staged lowering
+# (phases + scratch temporaries, codegen/lowering.py split_phases)
+# --------------------------------------------------------------------------------------
+
+
+def staged_forward_ij_temp(a: F64, out: F64):
+    with computation(FORWARD):
+        with interval(0, 1):
+            s = a
+        with interval(1, None):
+            s = s[0, 0, -1] * 0.5 + a
+    with computation(FORWARD), interval(...):
+        t = s * 2.0 + a
+        out = t[1, 0, 0] - t[-1, 0, 0] + t[0, 1, 0] * s
+
+
+case(
+    "staged_forward_ij_temp",
+    fields={"a": fs(12, 10, 6), "out": fs(10, 8, 6, init="zeros")},
+    origin={"a": (1, 1, 0), "out": (0, 0, 0)},
+    domain=(10, 8, 6),
+)(staged_forward_ij_temp)
+
+
+def staged_parallel_k_temp(a: F64, out: F64):
+    with computation(PARALLEL), interval(...):
+        tmp = a * 2.0 + 1.0
+    with computation(PARALLEL), interval(1, -1):
+        out = tmp[0, 0, 1] - a + tmp[0, 0, -1]
+
+
+case(
+    "staged_parallel_k_temp",
+    fields={"a": fs(7, 6, 8), "out": fs(7, 6, 8, init="zeros")},
+)(staged_parallel_k_temp)
+
+
+def staged_wide_halo(a: F64, out: F64):
+    with computation(PARALLEL), interval(...):
+        d = a[70, 0, 0] - a[-70, 0, 0]
+        out = d[0, 1, 0] + d[0, -1, 0] * 0.25
+
+
+case(
+    "staged_wide_halo",
+    fields={"a": fs(150, 7, 3), "out": fs(10, 5, 3, init="zeros")},
+    origin={"a": (70, 1, 0), "out": (0, 0, 0)},
+    domain=(10, 5, 3),
+)(staged_wide_halo)
