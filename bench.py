@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--jchunk", type=int, default=None)
+    ap.add_argument("--decomp", default="jstrips", choices=["jstrips", "2d"],
+                    help="N>1: J strips (default) or a balanced 2-D process grid (corners exchanged)")
     args = ap.parse_args()
 
     import torch
@@ -170,9 +172,15 @@ def main():
         import torch.distributed as dist
 
     from gt4py_amd import gtscript, storage
-    from gt4py_amd.distributed import HaloStencil
+    from gt4py_amd.distributed import Decomposition2D, HaloStencil, HaloStencil2D
 
     sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[args.config]
+    # weak scaling: the per-GPU tile is fixed, the global domain is ni x (nj * world)
+    global_ij = (ni, nj * world)
+    dec2d = None
+    if world > 1 and args.decomp == "2d":
+        dec2d = Decomposition2D.balanced(global_ij[0], global_ij[1], world)
+        ni, nj = dec2d.local_shape(rank)
     defs = stencil_defs()
     opts = {"device_sync": False}
     if args.jchunk:
@@ -202,7 +210,10 @@ def main():
             call_args = (fin, out)
             named = {"in_field": fin, "out_field": out}
             origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
-        if world > 1:
+        if dec2d is not None:
+            # 2-D tile: two-phase (corner-correct) exchange on the halo stream, interior overlapped
+            halo = HaloStencil2D(stencil, ["in_field"], dec2d, rank, (h, h))
+        elif world > 1:
             # J-strip of the global domain: exchange the in_field halo with the neighbours over
             # RCCL while the interior rows compute, then the two boundary strips
             halo = HaloStencil(stencil, ["in_field"], nj, h, rank, world)
@@ -251,7 +262,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
     cells_per_step = ni * nj * nk
-    total_cells = cells_per_step * args.steps * world
+    total_cells = global_ij[0] * global_ij[1] * nk * args.steps
     value = total_cells / elapsed / 1e6
     achieved_gbs = cells_per_step * bpc / (kernel_ms * 1e-3) / 1e9
     traffic = None
@@ -277,12 +288,19 @@ def main():
         "data": "synthetic (uniform random fields generated on device)",
         "config": {
             "workload": f"{sname} {ni}x{nj}x{nk} {np.dtype(dtype).name} per GPU"
-            + (f", J-strips of a {ni}x{nj * world}x{nk} global domain, RCCL halo {h}" if world > 1 else ""),
+            + (
+                f", {'J-strips' if dec2d is None else f'{dec2d.pi}x{dec2d.pj} tiles'} of a "
+                f"{global_ij[0]}x{global_ij[1]}x{nk} global domain, RCCL halo {h}"
+                if world > 1
+                else ""
+            ),
             "stencil": sname,
             "domain_per_gpu": [ni, nj, nk],
-            "global_domain": [ni, nj * world, nk],
+            "global_domain": [global_ij[0], global_ij[1], nk],
             "backend": "gt:mi355x",
-            "parallelism": f"ij-strips{world}" if world > 1 else "single",
+            "parallelism": (f"ij-strips{world}" if dec2d is None else f"ij-tiles{dec2d.pi}x{dec2d.pj}")
+            if world > 1
+            else "single",
         },
         "roofline": {
             "bound": "hbm",

@@ -109,3 +109,109 @@ def test_jstrips_cover_domain():
             assert b[0][0] == 0 and b[-1][1] == n
             assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
             assert max(s.size(r) for r in range(w)) - min(s.size(r) for r in range(w)) <= 1
+
+
+# ---------------------------------------------------------------------------------------
+# 2-D decomposition: corners, batching of several fields, periodic boundaries
+# ---------------------------------------------------------------------------------------
+
+
+def _worker2d(rank, world, port, outdir, pi, pj, periodic):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import stencil_cases as sc
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed import Decomposition2D, HaloStencil2D
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gin, gco = _global_inputs(periodic)
+    h = 2
+    nig, njg = gco.shape[:2]
+    dec = Decomposition2D(nig, njg, pi, pj, periodic)
+    (i0, i1), (j0, j1) = dec.bounds(rank)
+    ni, nj = i1 - i0, j1 - j0
+    lin = gin[i0 : i1 + 2 * h, j0 : j1 + 2 * h, :].copy()
+    ci, cj = dec.coords(rank)
+    # halo cells owned by another rank start as NaN: only the exchange may fill them
+    if ci > 0 or periodic[0]:
+        lin[:h] = np.nan
+    if ci < pi - 1 or periodic[0]:
+        lin[ni + h :] = np.nan
+    if cj > 0 or periodic[1]:
+        lin[:, :h] = np.nan
+    if cj < pj - 1 or periodic[1]:
+        lin[:, nj + h :] = np.nan
+    t_in = torch.from_numpy(lin)
+    t_in2 = torch.from_numpy(lin.copy() * 2.0)  # a second exchanged field (batched message)
+    t_out = torch.zeros((ni, nj, gin.shape[2]), dtype=torch.float64)
+    st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist2d.hdiff")
+    args = {"in_field": t_in, "out_field": t_out, "coeff": torch.from_numpy(gco[i0:i1, j0:j1, :].copy())}
+    origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    runner = HaloStencil2D(st, ["in_field"], dec, rank, (h, h))
+    runner(args, origin, (ni, nj, gin.shape[2]))
+    runner.ex.exchange([t_in2])
+    np.save(os.path.join(outdir, f"out_{rank}.npy"), t_out.numpy())
+    np.save(os.path.join(outdir, f"in_{rank}.npy"), t_in.numpy())
+    np.save(os.path.join(outdir, f"in2_{rank}.npy"), t_in2.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _global_inputs(periodic):
+    rng = np.random.default_rng(5)
+    nig, njg, nk, h = 13, 11, 3, 2
+    core = rng.uniform(-10, 10, (nig + 2 * h, njg + 2 * h, nk))
+    if periodic[0]:
+        core[:h] = core[nig : nig + h]
+        core[nig + h :] = core[h : 2 * h]
+    if periodic[1]:
+        core[:, :h] = core[:, njg : njg + h]
+        core[:, njg + h :] = core[:, h : 2 * h]
+    gco = rng.uniform(0, 0.5, (nig, njg, nk))
+    return core, gco
+
+
+@pytest.mark.parametrize(
+    "pi,pj,periodic",
+    [(2, 2, (False, False)), (3, 2, (False, False)), (2, 2, (True, True)), (1, 2, (True, False)), (2, 1, (False, True))],
+)
+def test_2d_decomposition_matches_single_domain(tmp_path, pi, pj, periodic):
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, REPO)
+    import stencil_cases as sc
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed import Decomposition2D
+
+    world = pi * pj
+    port = _free_port()
+    mp.spawn(_worker2d, args=(world, port, str(tmp_path), pi, pj, periodic), nprocs=world, join=True)
+    gin, gco = _global_inputs(periodic)
+    h = 2
+    nig, njg, nk = gco.shape
+    ref = np.zeros((nig, njg, nk))
+    st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist2d.hdiff")
+    st(gin.copy(), ref, gco, origin={"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)})
+    dec = Decomposition2D(nig, njg, pi, pj, periodic)
+    for r in range(world):
+        (i0, i1), (j0, j1) = dec.bounds(r)
+        assert np.array_equal(np.load(tmp_path / f"out_{r}.npy"), ref[i0:i1, j0:j1]), r
+        # halos incl. corners hold the owning ranks' cells (periodic images included)
+        assert np.array_equal(np.load(tmp_path / f"in_{r}.npy"), gin[i0 : i1 + 2 * h, j0 : j1 + 2 * h]), r
+        assert np.array_equal(np.load(tmp_path / f"in2_{r}.npy"), 2.0 * gin[i0 : i1 + 2 * h, j0 : j1 + 2 * h]), r
+
+
+def test_balanced_decomposition():
+    from gt4py_amd.distributed import Decomposition2D
+
+    d = Decomposition2D.balanced(8192, 8192, 8)
+    assert (d.pi, d.pj) in ((2, 4), (4, 2))
+    d = Decomposition2D.balanced(8192, 1024, 4)
+    assert (d.pi, d.pj) == (4, 1)
+    for r in range(d.size):
+        assert d.rank_of(*d.coords(r)) == r
