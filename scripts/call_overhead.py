@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Host cost of one gt:mi355x stencil call, layer by layer (tiny domain: launch-bound).
+
+    python scripts/call_overhead.py [--calls 3000]
+
+Prints one JSON line per layer: StencilObject.__call__ with validation, without, FrozenStencil,
+the launcher alone, and the bare ``gtmi_stencil_run`` ctypes call on pre-packed arguments.
+``device_sync=False`` everywhere: the number is host time per enqueued call.
+"""
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=3000)
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    from gt4py_amd import gtscript, storage
+
+    defs = bench.stencil_defs()
+    st = gtscript.stencil(backend="gt:mi355x", definition=defs[("horizontal_diffusion", np.float64)],
+                          name="overhead.hdiff", device_sync=False)
+    ni, nj, nk, h = 32, 16, 4, 2
+    fin = storage.from_array(np.random.default_rng(0).uniform(-1, 1, (ni + 2 * h, nj + 2 * h, nk)),
+                             backend="gt:mi355x", aligned_index=(h, h, 0))
+    out = storage.zeros((ni, nj, nk), np.float64, backend="gt:mi355x")
+    coeff = storage.full((ni, nj, nk), 0.1, np.float64, backend="gt:mi355x")
+    origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    dom = (ni, nj, nk)
+
+    def timeit(fn, n):
+        for _ in range(50):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        return (t1 - t0) / n * 1e6
+
+    class _Res(dict):
+        def __setitem__(self, k, v):
+            super().__setitem__(k, v)
+            print(json.dumps({"layer": k, "us_per_call": round(v, 2)}), flush=True)
+
+    res = _Res()
+    res["call_validate"] = timeit(lambda: st(fin, out, coeff, origin=origin, domain=dom), args.calls)
+    res["call_no_validate"] = timeit(
+        lambda: st(fin, out, coeff, origin=origin, domain=dom, validate_args=False), args.calls)
+    frozen = st.freeze(origin=origin, domain=dom)
+    res["frozen"] = timeit(lambda: frozen(in_field=fin, out_field=out, coeff=coeff), args.calls)
+    comp = [c.cell_contents for c in type(st).run.__closure__][0].compiled
+    launcher = comp.launcher
+    arrays = {"in_field": fin, "out_field": out, "coeff": coeff}
+    res["launcher"] = timeit(lambda: launcher(dom, origin, arrays, {}, device_sync=False), args.calls)
+    # bare ctypes call on pre-packed structs
+    lib = launcher.lib
+    fields, _ = launcher.pack_fields(dom, origin, arrays)
+    from gt4py_amd.runtime import ffi
+
+    scal = (ffi.GtmiScalar * 1)()
+    d3 = (ctypes.c_int64 * 3)(*dom)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res["ctypes_only"] = timeit(lambda: lib.run(d3, fields, launcher.n_fields, scal, 0, s), args.calls)
+    # GPU time of the tiny kernel itself, for scale
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(200):
+        lib.run(d3, fields, launcher.n_fields, scal, 0, s)
+    e1.record()
+    torch.cuda.synchronize()
+    res["gpu_us_per_launch_backtoback"] = e0.elapsed_time(e1) / 200 * 1e3
+
+
+if __name__ == "__main__":
+    main()

@@ -192,3 +192,24 @@ def test_scalar_fallback_layouts(name):
         stencil(**dev, **case.params, **kw)
     for k, v in outputs.items():
         gu.assert_match(storage.to_numpy(dev[k]), v, rtol=case.rtol, atol=case.atol, name=f"{name}:{k}")
+
+
+def test_packed_argument_cache_tracks_tensors():
+    """Re-allocated tensors (possibly at a recycled id) never reuse a stale packed pointer."""
+    _torch()
+    from gt4py_amd import gtscript, storage
+
+    st = gtscript.stencil(backend=BACKEND, definition=sc.copy_stencil, name="gpu.pack_cache")
+    keep = []
+    for trial in range(6):
+        a = storage.from_array(np.full((8, 6, 4), float(trial)), backend=BACKEND)
+        b = storage.zeros((8, 6, 4), np.float64, backend=BACKEND)
+        st(a, b, origin=(0, 0, 0), domain=(8, 6, 4))
+        assert (storage.to_numpy(b) == trial).all()
+        if trial % 2:
+            keep.append((a, b))  # alternate between fresh and surviving objects
+        del a, b
+    for trial, (a, b) in enumerate(keep):
+        a.fill_(100.0 + trial)
+        st(a, b, origin=(0, 0, 0), domain=(8, 6, 4), validate_args=False)
+        assert (storage.to_numpy(b) == 100.0 + trial).all()
