@@ -34,7 +34,7 @@ def generate_source(analysis, opts):
     lowered, components = lower_data_dims(analysis)
     abi = analysis.stencil.field_params()
     try:
-        plan = make_plan(lowered)
+        plan = make_plan(lowered, pointwise_plane=bool(opts.get("pointwise_plane", 1)))
         source, signature = hipgen.generate(lowered, plan, opts, abi_fields=abi, components=components)
     except UnsupportedStencil as direct_failure:
         # staged fallback: split computations into phases, column kernels + scratch temporaries
@@ -81,6 +81,7 @@ class Mi355xBackend(BaseBackend):
         "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
         "col_occupancy": {"versioning": True, "type": int, "description": "max column-kernel blocks per CU (0 = hw)"},
         "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
+        "pointwise_plane": {"versioning": True, "type": int, "description": "stream pointwise PARALLEL loops with K1"},
         "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow)"},
         "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},
         "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},

@@ -72,7 +72,17 @@ def _has_horizontal_offsets(vl: ir.VerticalLoop) -> bool:
     return False
 
 
-def make_plan(analysis: StencilAnalysis, column_only: bool = False) -> KernelPlan:
+def _pointwise_plane_ok(vl: ir.VerticalLoop) -> bool:
+    """A PARALLEL loop without horizontal offsets that K1 can stream (no value written and read at
+    a K offset, no run-time K offsets)."""
+    written = {a.name for a, w in _loop_accesses(vl) if w}
+    for a, w in _loop_accesses(vl):
+        if isinstance(a, ir.FieldAccess) and (a.k_offset is not None or (not w and a.name in written and a.offset[2])):
+            return False
+    return True
+
+
+def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_plane: bool = False) -> KernelPlan:
     """``column_only``: every computation runs in column kernels (the staged fallback, after
     ``lowering.split_phases``); otherwise PARALLEL computations with horizontal offsets become
     J-streaming plane kernels."""
@@ -91,7 +101,10 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False) -> KernelPla
 
     run_written: Set[str] = set()
     for li, vl in enumerate(st.vertical_loops):
-        if not column_only and vl.loop_order == ir.LoopOrder.PARALLEL and _has_horizontal_offsets(vl):
+        plane = vl.loop_order == ir.LoopOrder.PARALLEL and (
+            _has_horizontal_offsets(vl) or (pointwise_plane and _pointwise_plane_ok(vl))
+        )
+        if not column_only and plane:
             if any(isinstance(a, ir.FieldAccess) and a.k_offset is not None for a, _ in _loop_accesses(vl)):
                 raise UnsupportedStencil("run-time K offsets in a PARALLEL computation with horizontal offsets")
             flush()
