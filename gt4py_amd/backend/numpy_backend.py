@@ -136,8 +136,7 @@ class NumpyExecutor:
                         full[d] = next(it)
                 fields[p.name] = _Arr(arr, full, mask)
             else:
-                if v is not None:
-                    scalars[p.name] = p.dtype.np_dtype.type(v)
+                scalars[p.name] = None if v is None else p.dtype.np_dtype.type(v)
         for t in st.temporaries:
             (ilo, ihi), (jlo, jhi) = self.analysis.extents.fields.get(t.name, ((0, 0), (0, 0)))
             arr = np.zeros((ni + ilo + ihi, nj + jlo + jhi, nk) + tuple(t.data_dims), dtype=t.dtype.np_dtype)
@@ -279,11 +278,13 @@ class NumpyExecutor:
                 raise NotImplementedError("field-valued data index in an assignment target")
             idx = tuple(idx) + tuple(didx)
         cur = f.array[idx]
-        val = np.broadcast_to(value, cur.shape) if cur.shape == value.shape or not all(f.mask) else value
-        if not all(f.mask):
-            val = np.broadcast_to(value, _shape(creg))[tuple(slice(None) if m else 0 for m in f.mask)]
+        if all(f.mask):
+            val = np.broadcast_to(value, cur.shape)
+        else:  # lower-dimensional target: the (broadcast) values of the missing axis collapse
+            sel = tuple(slice(None) if m else 0 for m in f.mask)
+            val = np.broadcast_to(value, _shape(creg))[sel]
             if mask is not None:
-                mask = mask[tuple(slice(None) if m else 0 for m in f.mask)]
+                mask = mask[sel]
         f.array[idx] = val if mask is None else np.where(mask, val, cur)
 
     def _assign(self, s: ir.Assign, reg, mask):
@@ -325,7 +326,10 @@ class NumpyExecutor:
         if isinstance(e, ir.Literal):
             return e.dtype.np_dtype.type(e.value)
         if isinstance(e, ir.ScalarAccess):
-            return self.scalars[e.name]
+            v = self.scalars.get(e.name)
+            if v is None:
+                raise TypeError(f"The type of parameter '{e.name}' is '{type(None)}' instead of '{e.dtype.np_dtype}'")
+            return v
         if isinstance(e, ir.FieldAccess):
             f = self.fields[e.name]
             if e.k_offset is not None:

@@ -1313,6 +1313,11 @@ def generate(
         launches.append(hs)
     import json
 
+    used_scalars = {
+        n.name for vl in st.vertical_loops for sec in vl.sections for n in ir.walk(sec.body) if isinstance(n, ir.ScalarAccess)
+    }
+    for comp in components.values():
+        used_scalars |= {n.name for x in comp.index for n in ir.walk(x) if isinstance(n, ir.ScalarAccess)}
     signature = {
         "abi": 2,
         "fields": [
@@ -1323,7 +1328,9 @@ def generate(
             {"name": t, "dtype": st.decl(t).dtype.name.lower(), "extent": [list(e) for e in plan.scratch_extent[t]]}
             for t in plan.scratch
         ],
-        "scalars": [{"name": s.name, "dtype": s.dtype.name.lower()} for s in st.scalar_params()],
+        "scalars": [
+            {"name": s.name, "dtype": s.dtype.name.lower(), "used": s.name in used_scalars} for s in st.scalar_params()
+        ],
         "kernels": [type(k).__name__ for k in plan.kernels],
     }
     sig_json = json.dumps(signature).replace("\\", "\\\\").replace('"', '\\"')

@@ -203,6 +203,10 @@ class StencilLauncher:
         scalars = (ffi.GtmiScalar * max(1, n_sc))()
         for j, s in enumerate(self.scalars):
             v = params.get(s["name"])
+            if v is None and s.get("used", True):
+                raise TypeError(
+                    f"The type of parameter '{s['name']}' is '{type(v)}' instead of '{np.dtype(s['dtype'])}'"
+                )
             ffi.set_scalar(scalars[j], s["dtype"], 0 if v is None else v)
         dom = (ctypes.c_int64 * 3)(ni, nj, nk)
         if device.index is not None and device.index != torch.cuda.current_device():

@@ -443,11 +443,16 @@ def make_stencil_class(
     param_names = [n for n in sig.parameters if n in parameter_info]
     parts = []
     seen_kwonly = False
+    ns: Dict[str, Any] = {}
     for p in sig.parameters.values():
         if p.kind == p.KEYWORD_ONLY and not seen_kwonly:
             parts.append("*")
             seen_kwonly = True
-        parts.append(f"{p.name}=None" if p.default is None else p.name)
+        if p.default is inspect.Parameter.empty:
+            parts.append(p.name)
+        else:  # the definition's default value (module_generator.py:258-284)
+            ns[f"_default_{p.name}"] = p.default
+            parts.append(f"{p.name}=_default_{p.name}")
     if not seen_kwonly:
         parts.append("*")
     parts += ["domain=None", "origin=None", "validate_args=True", "exec_info=None"]
@@ -457,7 +462,6 @@ def make_stencil_class(
         f"def __call__(self, {', '.join(parts)}):\n"
         f"    self._call_impl(dict({fdict}), dict({pdict}), domain, origin, validate_args, exec_info)\n"
     )
-    ns: Dict[str, Any] = {}
     exec(compile(src, f"<gt4py_amd:{class_name}.__call__>", "exec"), ns)  # noqa: S102 - generated code
 
     def run(self, _domain_, _origin_, exec_info, **kwargs):
