@@ -139,8 +139,10 @@ class NumpyExecutor:
                 scalars[p.name] = None if v is None else p.dtype.np_dtype.type(v)
         for t in st.temporaries:
             (ilo, ihi), (jlo, jhi) = self.analysis.extents.fields.get(t.name, ((0, 0), (0, 0)))
-            arr = np.zeros((ni + ilo + ihi, nj + jlo + jhi, nk) + tuple(t.data_dims), dtype=t.dtype.np_dtype)
-            fields[t.name] = _Arr(arr, (ilo, jlo, 0), (True, True, True))
+            mask = t.mask
+            shape = [n for n, m in zip((ni + ilo + ihi, nj + jlo + jhi, nk), mask) if m]
+            arr = np.zeros(tuple(shape) + tuple(t.data_dims), dtype=t.dtype.np_dtype)
+            fields[t.name] = _Arr(arr, (ilo, jlo, 0), mask)
         self.fields, self.scalars, self.domain = fields, scalars, (ni, nj, nk)
         self.api = {p.name for p in st.field_params()}
         with np.errstate(divide="ignore", over="ignore", under="ignore", invalid="ignore"):

@@ -311,6 +311,11 @@ class PlaneGen:
         self.opts = opts
         self.vl = self.st.vertical_loops[kernel.loop]
         self.sec = self.vl.sections[kernel.section]
+        for acc, w in iter_accesses(self.sec.body):
+            if isinstance(acc, ir.FieldAccess) and w and not self.st.decl(acc.name).mask[2]:
+                # one value per column written from every level of a PARALLEL section: only a
+                # sequential column sweep defines which level is the last writer
+                raise UnsupportedStencil(f"'{acc.name}' has no K axis and is written in a PARALLEL section")
         self.vals: List[Val] = []
         self.loads: Dict[Tuple[str, int], Val] = {}
         self.current: Dict[str, Val] = {}
@@ -1325,7 +1330,12 @@ def generate(
             for p in abi_fields
         ],
         "scratch": [
-            {"name": t, "dtype": st.decl(t).dtype.name.lower(), "extent": [list(e) for e in plan.scratch_extent[t]]}
+            {
+                "name": t,
+                "dtype": st.decl(t).dtype.name.lower(),
+                "extent": [list(e) for e in plan.scratch_extent[t]],
+                "axes": list(st.decl(t).axes),
+            }
             for t in plan.scratch
         ],
         "scalars": [

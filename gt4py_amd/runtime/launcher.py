@@ -88,8 +88,12 @@ class StencilLauncher:
                 (ilo, ihi), (jlo, jhi) = s["extent"]
                 si, sj = ni + ilo + ihi, nj + jlo + jhi
                 pi = -(-si // 32) * 32
-                buf = torch.empty(pi * sj * nk, dtype=torch_dtype(np.dtype(s["dtype"])), device=device)
-                out.append((buf, (si, sj, nk), (1, pi, pi * sj), (ilo, jlo, 0), s["dtype"]))
+                if "K" in s.get("axes", ("I", "J", "K")):
+                    buf = torch.empty(pi * sj * nk, dtype=torch_dtype(np.dtype(s["dtype"])), device=device)
+                    out.append((buf, (si, sj, nk), (1, pi, pi * sj), (ilo, jlo, 0), s["dtype"]))
+                else:  # IJ temporary: one plane shared by every level (K stride 0)
+                    buf = torch.empty(pi * sj, dtype=torch_dtype(np.dtype(s["dtype"])), device=device)
+                    out.append((buf, (si, sj, 1), (1, pi, 0), (ilo, jlo, 0), s["dtype"]))
             self._scratch_cache[key] = out
         return self._scratch_cache[key]
 

@@ -27,6 +27,7 @@ from gt4py_amd.gtscript import (
     BACKWARD,
     FORWARD,
     PARALLEL,
+    IJ,
     Field,
     I,
     J,
@@ -1890,3 +1891,40 @@ case(
     origin={"a": (70, 1, 0), "out": (0, 0, 0)},
     domain=(10, 5, 3),
 )(staged_wide_halo)
+
+
+# --------------------------------------------------------------------------------------
+# Iterator access and 2-D temporaries (test_code_generation.py:1350-1383, 1536-1590):
+# reference numpy-backend features; gt:mi355x supports iterator access, and raises for 2-D
+# temporaries exactly like the reference's gt:* backends
+# --------------------------------------------------------------------------------------
+
+
+def iterator_access(field_A: F64, field_B: F64, offsets: Field[gtscript.K, np.int32]):
+    with computation(PARALLEL), interval(...):
+        if K == 2:  # noqa: F821
+            field_A = 20.20
+        field_B = float(K + offsets)  # noqa: F821
+
+
+case(
+    "iterator_access",
+    fields={"field_A": fs(3, 4, 5, init="zeros"), "field_B": fs(3, 4, 5, init="zeros"),
+            "offsets": fs(5, dtype="i4", init=("int", -3, 3))},
+)(iterator_access)
+
+
+def temporaries_2d(in_field: F64, out_field: F64):
+    with computation(FORWARD), interval(0, 1):
+        tmp_2D: Field[IJ, np.float64] = 0
+    with computation(FORWARD), interval(...):
+        tmp_2D = tmp_2D + in_field
+    with computation(FORWARD), interval(...):
+        out_field = tmp_2D
+
+
+case(
+    "temporaries_2d",
+    fields={"in_field": fs(5, 5, 3), "out_field": fs(5, 5, 3, init="zeros")},
+    features=("numpy_only",),
+)(temporaries_2d)
