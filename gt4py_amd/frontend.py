@@ -20,6 +20,7 @@ Literal precision follows ``literal_int_precision``/``literal_float_precision``
 from __future__ import annotations
 
 import ast
+import dataclasses
 import builtins
 import inspect
 import itertools
@@ -854,7 +855,36 @@ class StencilParser:
             return self._parse_call(node, scope, pre)
         raise GTScriptSyntaxError(f"Unsupported expression {type(node).__name__}")
 
+    def _absolute_k(self, node: ast.Call, scope: _Scope, pre) -> ir.Expr:
+        """``field.at(K=expr[, ddim=[...]])``: the field at absolute level ``expr`` (relative to the
+        field's origin) -- lowered to a run-time K offset ``expr - K`` of the current level
+        (reference ``gtscript_frontend.py:1660-1711``, AbsoluteKIndex)."""
+        kws = node.keywords
+        if node.args or not kws or kws[0].arg != "K" or len(kws) > 2 or (len(kws) == 2 and kws[1].arg != "ddim"):
+            raise GTScriptSyntaxError(
+                "Absolute K index: Bad syntax. Must be of the form `.at(K=..., ddim=[...])` "
+            )
+        kval = self._parse_expr(kws[0].value, scope, pre)
+        if isinstance(kval, ir.AxisIndex):
+            raise GTScriptSyntaxError("Absolute K index: bad syntax, you cannot use an axis iterator in `.at(K=...)`")
+        didx = None
+        if len(kws) == 2:
+            if not isinstance(kws[1].value, (ast.List, ast.Tuple)):
+                raise GTScriptSyntaxError("Absolute K index: `ddim` must be a list of values")
+            didx = self._parse_data_index(ast.Tuple(elts=kws[1].value.elts, ctx=ast.Load()), scope, pre)
+        base = node.func.value
+        if not isinstance(base, ast.Name) or self._decl_of(base.id, scope) is None:
+            raise GTScriptSyntaxError("Absolute K index: `.at` needs a field")
+        decl = self._decl_of(base.id, scope)
+        if not decl.mask[2]:
+            raise GTScriptSyntaxError("Tried accessing a field with no K-dimensions with an absolute K-index.")
+        acc = self._resolve_name(base.id, scope, (0, 0, 0), didx)
+        koff = ir.BinaryOp("-", ir.NativeCall("int64", [kval]), ir.AxisIndex(2))
+        return dataclasses.replace(acc, k_offset=koff)
+
     def _parse_call(self, node: ast.Call, scope: _Scope, pre) -> ir.Expr:
+        if isinstance(node.func, ast.Attribute) and node.func.attr == "at":
+            return self._absolute_k(node, scope, pre)
         fname = self._call_name(node)
         func_obj = None
         if isinstance(node.func, ast.Name):

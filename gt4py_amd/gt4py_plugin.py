@@ -67,8 +67,11 @@ def _expr(node) -> ir.Expr:
         didx = [_expr(x) for x in (node.data_index or [])]
         if isinstance(off, gtir.VariableKOffset):
             return ir.FieldAccess(node.name, (0, 0, 0), _dt(node.dtype), didx, _expr(off.k))
+        if isinstance(off, gtir.AbsoluteKIndex):
+            koff = ir.BinaryOp("-", ir.NativeCall("int64", [_expr(off.k)]), ir.AxisIndex(2))
+            return ir.FieldAccess(node.name, (0, 0, 0), _dt(node.dtype), didx, koff)
         if not hasattr(off, "i"):
-            raise NotImplementedError("absolute K indexing is not supported by gt:mi355x")
+            raise NotImplementedError(f"GTIR offset {type(off).__name__}")
         return ir.FieldAccess(node.name, (int(off.i), int(off.j), int(off.k)), _dt(node.dtype), didx)
     if isinstance(node, gtir.ScalarAccess):
         return ir.ScalarAccess(node.name, _dt(node.dtype))

@@ -1928,3 +1928,67 @@ case(
     fields={"in_field": fs(5, 5, 3), "out_field": fs(5, 5, 3, init="zeros")},
     features=("numpy_only",),
 )(temporaries_2d)
+
+
+# --------------------------------------------------------------------------------------
+# Absolute K indexing `field.at(K=...)` (test_code_generation.py:1240-1347); fixtures from the
+# reference debug backend (its numpy backend raises NotImplementedError for this feature)
+# --------------------------------------------------------------------------------------
+
+
+def abs_k_literal(in_field: F64, out_field: F64):
+    with computation(PARALLEL), interval(...):
+        out_field = in_field.at(K=2)
+
+
+case("abs_k_literal", fields={"in_field": fs(5, 4, 6), "out_field": fs(5, 4, 6, init="zeros")},
+     features=("golden_debug",))(abs_k_literal)
+
+
+def abs_k_param(in_field: F64, out_field: F64, idx: int):
+    with computation(PARALLEL), interval(...):
+        out_field = in_field.at(K=idx) + in_field.at(K=idx - 1)
+
+
+case("abs_k_param", fields={"in_field": fs(5, 4, 6), "out_field": fs(5, 4, 6, init="zeros")},
+     params={"idx": 3}, features=("golden_debug",))(abs_k_param)
+
+
+def abs_k_field(in_field: F64, index_field: Field[IJ, np.int64], out_field: F64):
+    with computation(PARALLEL), interval(...):
+        out_field = in_field.at(K=index_field)
+
+
+case("abs_k_field", fields={"in_field": fs(5, 4, 6), "index_field": fs(5, 4, dtype="i8", init=("int", 0, 6)),
+                            "out_field": fs(5, 4, 6, init="zeros")}, features=("golden_debug",))(abs_k_field)
+
+
+def abs_k_field_computation(in_field: F64, index_field: Field[IJ, np.int32], out_field: F64):
+    with computation(FORWARD), interval(...):
+        out_field = in_field.at(K=index_field - 1) * 2.0
+
+
+case("abs_k_field_computation",
+     fields={"in_field": fs(5, 4, 6), "index_field": fs(5, 4, dtype="i4", init=("int", 1, 7)),
+             "out_field": fs(5, 4, 6, init="zeros")}, features=("golden_debug",))(abs_k_field_computation)
+
+
+def abs_k_lowdim(k_field: F1DK, out_field: F64):
+    with computation(PARALLEL), interval(...):
+        out_field = k_field.at(K=2)
+
+
+case("abs_k_lowdim", fields={"k_field": fs(6), "out_field": fs(5, 4, 6, init="zeros")},
+     features=("golden_debug",))(abs_k_lowdim)
+
+
+def abs_k_conditional(in_field: F64, out_field: F64):
+    with computation(PARALLEL), interval(...):
+        k_level = 0
+        while in_field.at(K=k_level) < 2:
+            k_level += 1
+        out_field[0, 0, 0] = k_level
+
+
+case("abs_k_conditional", fields={"in_field": fs(5, 4, 6, init=("ramp", -5.0, 5.0)), "out_field": fs(5, 4, 6, init="zeros")},
+     features=("golden_debug",))(abs_k_conditional)
