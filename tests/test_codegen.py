@@ -57,3 +57,24 @@ def _lib_path(stencil):
         if comp is not None:
             return comp.lib_path
     raise AssertionError("no compiled library attached")
+
+
+@pytest.mark.parametrize("name", ["hdiff_f64", "tridiag", "higher_dimensional_fields", "staged_forward_ij_temp"])
+def test_library_loads_and_describes_itself(name):
+    """The C-ABI library dlopens on a host without a GPU (no compute call is made), reports the
+    ABI version of include/gtmi.h and a signature that matches the stencil's API."""
+    case = sc.CASES[name]
+    stencil = gtscript.stencil(backend="gt:mi355x", definition=case.definition, externals=case.externals,
+                               name=f"gpu.{name}")
+    lib = ffi.load_library(_lib_path(stencil))
+    assert lib.lib.gtmi_abi_version() == ffi.GTMI_ABI_VERSION == 2
+    sig = lib.signature
+    assert sig["abi"] == 2
+    assert [f["name"] for f in sig["fields"]] == list(stencil.field_info.keys())
+    for f in sig["fields"]:
+        fi = stencil.field_info[f["name"]]
+        assert tuple(f["axes"]) == tuple(fi.axes) and tuple(f["data_dims"]) == tuple(fi.data_dims)
+    assert [s["name"] for s in sig["scalars"]] == list(stencil.parameter_info.keys())
+    assert lib.last_error() == ""
+    with open(HEADER) as fh:
+        assert f"#define GTMI_ABI_VERSION {ffi.GTMI_ABI_VERSION}" in fh.read()
