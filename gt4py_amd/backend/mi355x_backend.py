@@ -81,6 +81,7 @@ class Mi355xBackend(BaseBackend):
         "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
         "col_occupancy": {"versioning": True, "type": int, "description": "max column-kernel blocks per CU (0 = hw)"},
         "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
+        "min_blocks": {"versioning": True, "type": int, "description": "plane kernels: __launch_bounds__ min blocks per CU"},
         "pointwise_plane": {"versioning": True, "type": int, "description": "stream pointwise PARALLEL loops with K1"},
         "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow)"},
         "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},

@@ -539,7 +539,9 @@ class PlaneGen:
             L.append("};")
             L.append("")
         kname = f"k{k}_plane_v{V}"
-        L.append(f"__global__ void __launch_bounds__({WAVE * PLANE_BLOCK_WAVES}) {kname}(const K{k}Params p) {{")
+        mb = int(self.opts.get("min_blocks", 0))  # blocks per CU the register budget must allow
+        lb = f"{WAVE * PLANE_BLOCK_WAVES}, {mb}" if mb > 0 else f"{WAVE * PLANE_BLOCK_WAVES}"
+        L.append(f"__global__ void __launch_bounds__({lb}) {kname}(const K{k}Params p) {{")
         B = []
         B.append("const int lane = (int)__lane_id();")
         B.append("const int wave = (int)(threadIdx.x >> 6);")

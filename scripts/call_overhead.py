@@ -76,6 +76,15 @@ def main():
     d3 = (ctypes.c_int64 * 3)(*dom)
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res["ctypes_only"] = timeit(lambda: lib.run(d3, fields, launcher.n_fields, scal, 0, s), args.calls)
+    # a captured HIP graph of 10 calls, per call
+    from gt4py_amd.runtime.graph import StencilGraph
+
+    def ten():
+        for _ in range(10):
+            st(fin, out, coeff, origin=origin, domain=dom, validate_args=False)
+
+    g = StencilGraph(ten)
+    res["graph_replay_per_call"] = timeit(g.replay, max(1, args.calls // 10)) / 10
     # GPU time of the tiny kernel itself, for scale
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
