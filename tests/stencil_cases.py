@@ -1992,3 +1992,65 @@ def abs_k_conditional(in_field: F64, out_field: F64):
 
 case("abs_k_conditional", fields={"in_field": fs(5, 4, 6, init=("ramp", -5.0, 5.0)), "out_field": fs(5, 4, 6, init="zeros")},
      features=("golden_debug",))(abs_k_conditional)
+
+
+# --------------------------------------------------------------------------------------
+# Remaining stencil_definitions.py programs: every data type, a region with a conditional
+# --------------------------------------------------------------------------------------
+
+
+def data_types(
+    bool_field: Field[bool],
+    npbool_field: Field[np.bool_],
+    int_field: Field[int],
+    int8_field: Field[np.int8],
+    int16_field: Field[np.int16],
+    int32_field: Field[np.int32],
+    int64_field: Field[np.int64],
+    float_field: Field[float],
+    float32_field: Field[np.float32],
+    float64_field: Field[np.float64],
+):
+    with computation(PARALLEL), interval(...):
+        bool_field = True
+        npbool_field = False
+        int_field = 2147483647
+        int8_field = 127
+        int16_field = 32767
+        int32_field = 2147483647
+        int64_field = 9223372036854775807
+        float_field = 37.5
+        float32_field = 37.5
+        float64_field = 37.5
+
+
+case(
+    "data_types",
+    fields={
+        "bool_field": fs(4, 3, 2, dtype="?", init="bool"),
+        "npbool_field": fs(4, 3, 2, dtype="?", init="bool"),
+        "int_field": fs(4, 3, 2, dtype="i8", init=("int", -9, 9)),
+        "int8_field": fs(4, 3, 2, dtype="i1", init=("int", -9, 9)),
+        "int16_field": fs(4, 3, 2, dtype="i2", init=("int", -9, 9)),
+        "int32_field": fs(4, 3, 2, dtype="i4", init=("int", -9, 9)),
+        "int64_field": fs(4, 3, 2, dtype="i8", init=("int", -9, 9)),
+        "float_field": fs(4, 3, 2),
+        "float32_field": fs(4, 3, 2, dtype="f4"),
+        "float64_field": fs(4, 3, 2),
+    },
+)(data_types)
+
+
+def horizontal_region_with_conditional(field_in: F64, field_out: F64):
+    with computation(PARALLEL), interval(...):
+        with horizontal(region[I[0] : I[0] + 2, J[0] : J[0] + 2], region[I[-1] - 2 : I[-1], J[-1] - 2 : J[-1]]):
+            if field_in > 0:
+                field_out = field_in + 1.0
+            else:
+                field_out = 0
+
+
+case(
+    "horizontal_region_with_conditional",
+    fields={"field_in": fs(7, 6, 3), "field_out": fs(7, 6, 3, init=("const", 42.0))},
+)(horizontal_region_with_conditional)
