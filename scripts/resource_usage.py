@@ -30,7 +30,8 @@ def main():
     from gt4py_amd.loader import StencilBuilder
 
     b = StencilBuilder(bench.stencil_defs()[(sname, dtype)], from_name("gt:mi355x"),
-                       BuildOptions(name=f"resources.{cfg}", module="resources", backend_opts=opts), {}, {})
+                       BuildOptions(name=f"resources.{cfg}", module="resources", backend_opts=opts),
+                       bench.EXTERNALS.get(sname, {}), {})
     source, _ = hipgen.generate(b.analysis, make_plan(b.analysis), opts)
     lib = jit.compile_source(source)
     src = os.path.join(os.path.dirname(lib), "stencil.hip")

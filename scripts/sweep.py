@@ -50,7 +50,8 @@ def main():
     stencils = []
     for i, v in enumerate(variants):
         stencils.append(
-            gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"sweep.{args.config}.{i}", device_sync=False, **v)
+            gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"sweep.{args.config}.{i}", device_sync=False,
+                             externals=bench.EXTERNALS.get(sname, {}), **v)
         )
     if args.build_only:
         print(f"built {len(stencils)} variants")
