@@ -54,3 +54,20 @@ def test_field_info_matches_reference(name):
         pi = stencil.parameter_info[pname]
         assert int(pi.access) == ref["access"] and str(pi.dtype) == ref["dtype"], pname
     assert stencil.domain_info.min_sequential_axis_size == meta["domain_info"]["min_sequential_axis_size"]
+
+
+def test_c1_copy_config_numpy_backend():
+    """BASELINE.json configs[0]: copy_stencil 128x128x64 f64 through the CPU (numpy) path, bit-exact."""
+    import time
+
+    from gt4py_amd import gtscript, storage
+
+    st = gtscript.stencil(backend="numpy", definition=sc.copy_stencil, name="c1.copy")
+    a = storage.from_array(np.random.default_rng(0).random((128, 128, 64)), backend="numpy")
+    b = storage.zeros((128, 128, 64), np.float64, backend="numpy")
+    st(a, b, origin=(0, 0, 0), domain=(128, 128, 64))
+    t0 = time.perf_counter()
+    st(a, b, origin=(0, 0, 0), domain=(128, 128, 64), validate_args=False)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(np.asarray(b), np.asarray(a))
+    assert dt < 5.0
