@@ -94,7 +94,11 @@ def _backend_name(group=None) -> str:
 class HaloExchange2D:
     """Two-phase, batched halo exchange of ``[ni+2hi, nj+2hj, nk]`` fields."""
 
-    def __init__(self, decomp: Decomposition2D, rank: int, halo: Tuple[int, int], group=None):
+    def __init__(self, decomp: Decomposition2D, rank: int, halo: Tuple[int, int], group=None,
+                 force_comm: bool = False):
+        """``force_comm``: send to oneself through the communicator instead of copying locally
+        (a periodic axis with one rank); lets one GPU exercise the RCCL path end to end."""
+        self.force_comm = force_comm
         self.d = decomp
         self.rank = rank
         self.hi, self.hj = halo
@@ -160,14 +164,15 @@ class HaloExchange2D:
         # order of the receives, so that with two ranks on a periodic axis (W and E are the same
         # peer) the k-th receive from a peer matches that peer's k-th send.
         ops, unpack = [], []
+        local = lambda peer: peer == self.rank and not self.force_comm  # noqa: E731
         for d in reversed(dirs):
             peer = self.nbr[d]
-            if peer != self.rank:
+            if not local(peer):
                 gpeer = dist.get_global_rank(self.group, peer) if self.group is not None else peer
                 ops.append(dist.P2POp(dist.isend, sbuf[d], gpeer, self.group))
         for d in dirs:
             peer = self.nbr[d]
-            if peer == self.rank:  # periodic axis with one rank: my own opposite face
+            if local(peer):  # periodic axis with one rank: my own opposite face
                 unpack.append((d, sbuf[self._OPPOSITE[d]]))
                 continue
             gpeer = dist.get_global_rank(self.group, peer) if self.group is not None else peer
@@ -205,13 +210,15 @@ class HaloStencil2D:
     """
 
     def __init__(self, stencil, halo_fields: Sequence[str], decomp: Decomposition2D, rank: int,
-                 halo: Tuple[int, int], group=None, overlap: bool = True):
+                 halo: Tuple[int, int], group=None, overlap: bool = True, force_comm: bool = False):
         self.stencil = stencil
         self.halo_fields = list(halo_fields)
-        self.ex = HaloExchange2D(decomp, rank, halo, group)
+        self.ex = HaloExchange2D(decomp, rank, halo, group, force_comm=force_comm)
         self.hi, self.hj = halo
         self.ni, self.nj = decomp.local_shape(rank)
-        self.overlap = overlap and decomp.size > 1 and self.ni > 2 * self.hi and self.nj > 2 * self.hj
+        self.overlap = (
+            overlap and (decomp.size > 1 or force_comm) and self.ni > 2 * self.hi and self.nj > 2 * self.hj
+        )
         self._stream = None
 
     def _run(self, kw, origin, i0, j0, ni, nj, nk):

@@ -56,14 +56,23 @@ class JHaloExchange:
     is left untouched (it holds the global boundary input).
     """
 
-    def __init__(self, nj_local: int, halo: int, rank: int, world_size: int, group=None):
+    def __init__(self, nj_local: int, halo: int, rank: int, world_size: int, group=None,
+                 periodic: bool = False, force_comm: bool = False):
+        """``periodic``: the J axis wraps (ranks 0 and N-1 are neighbours; one rank copies its own
+        faces). ``force_comm``: a rank that is its own neighbour still goes through the
+        communicator (one GPU can exercise the RCCL path end to end)."""
         self.nj = nj_local
         self.h = halo
         self.rank = rank
         self.world = world_size
         self.group = group
-        self.prev = rank - 1 if rank > 0 else None
-        self.next = rank + 1 if rank < world_size - 1 else None
+        self.force_comm = force_comm
+        if periodic:
+            self.prev = (rank - 1) % world_size
+            self.next = (rank + 1) % world_size
+        else:
+            self.prev = rank - 1 if rank > 0 else None
+            self.next = rank + 1 if rank < world_size - 1 else None
         self._bufs: Dict[Tuple, Dict] = {}
         self._pending: List = []
         self._stage_host: Optional[bool] = None
@@ -85,26 +94,43 @@ class JHaloExchange:
         return self._bufs[key]
 
     def start(self, fields: Sequence) -> List:
-        """Pack faces and post the sends/receives; returns the pending work handles."""
+        """Pack faces and post the sends/receives; returns the pending work handles.
+
+        Every send is posted before every receive, sends hi-face first and receives lo-halo
+        first: with one peer on both sides (two ranks on a periodic axis, or one rank and
+        ``force_comm``) the k-th receive from a peer then matches that peer's k-th send.
+        """
         import torch.distributed as dist
 
         if self._stage_host is None:
             # gloo moves host memory only: stage device faces through the host (tests / CPU runs)
             self._stage_host = _backend_name(self.group) == "gloo"
-        ops = []
         h, nj = self.h, self.nj
         self._pending = []
+        sends, recvs = [], []
+        local = lambda peer: peer == self.rank and not self.force_comm  # noqa: E731
         for t in fields:
             b = self._buffers(t)
-            if self.prev is not None:
-                b["send_lo"].copy_(t[:, h : 2 * h, :])
-                ops.append(dist.P2POp(dist.isend, b["send_lo"], self._global_rank(self.prev), self.group))
-                ops.append(dist.P2POp(dist.irecv, b["recv_lo"], self._global_rank(self.prev), self.group))
             if self.next is not None:
                 b["send_hi"].copy_(t[:, nj : nj + h, :])
-                ops.append(dist.P2POp(dist.isend, b["send_hi"], self._global_rank(self.next), self.group))
-                ops.append(dist.P2POp(dist.irecv, b["recv_hi"], self._global_rank(self.next), self.group))
+            if self.prev is not None:
+                b["send_lo"].copy_(t[:, h : 2 * h, :])
+            if self.next is not None and not local(self.next):
+                sends.append(dist.P2POp(dist.isend, b["send_hi"], self._global_rank(self.next), self.group))
+            if self.prev is not None and not local(self.prev):
+                sends.append(dist.P2POp(dist.isend, b["send_lo"], self._global_rank(self.prev), self.group))
+            if self.prev is not None:
+                if local(self.prev):
+                    b["recv_lo"].copy_(b["send_hi"])
+                else:
+                    recvs.append(dist.P2POp(dist.irecv, b["recv_lo"], self._global_rank(self.prev), self.group))
+            if self.next is not None:
+                if local(self.next):
+                    b["recv_hi"].copy_(b["send_lo"])
+                else:
+                    recvs.append(dist.P2POp(dist.irecv, b["recv_hi"], self._global_rank(self.next), self.group))
             self._pending.append((t, b))
+        ops = sends + recvs
         if not ops:
             return []
         return dist.batch_isend_irecv(ops)
@@ -134,13 +160,13 @@ class HaloStencil:
     """
 
     def __init__(self, stencil, halo_fields: Sequence[str], nj_local: int, halo: int, rank: int, world_size: int,
-                 group=None, overlap: bool = True):
+                 group=None, overlap: bool = True, periodic: bool = False, force_comm: bool = False):
         self.stencil = stencil
         self.halo_fields = list(halo_fields)
-        self.exchange = JHaloExchange(nj_local, halo, rank, world_size, group)
+        self.exchange = JHaloExchange(nj_local, halo, rank, world_size, group, periodic, force_comm)
         self.h = halo
         self.nj = nj_local
-        self.overlap = overlap and world_size > 1 and nj_local > 2 * halo
+        self.overlap = overlap and (world_size > 1 or force_comm) and nj_local > 2 * halo
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}

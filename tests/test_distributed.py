@@ -215,3 +215,56 @@ def test_balanced_decomposition():
     assert (d.pi, d.pj) == (4, 1)
     for r in range(d.size):
         assert d.rank_of(*d.coords(r)) == r
+
+
+def _worker1d_periodic(rank, world, port, outdir):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import stencil_cases as sc
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed import HaloStencil, JStrips
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gin, gco = _global_inputs((False, True))
+    h = 2
+    nig, njg, nk = gco.shape
+    j0, j1 = JStrips(njg, world).bounds(rank)
+    nj = j1 - j0
+    lin = gin[:, j0 : j1 + 2 * h, :].copy()
+    lin[:, :h] = np.nan  # every J halo is owned by a (periodic) neighbour
+    lin[:, nj + h :] = np.nan
+    t_in = torch.from_numpy(lin)
+    t_out = torch.zeros((nig, nj, nk), dtype=torch.float64)
+    st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist1dp.hdiff")
+    args = {"in_field": t_in, "out_field": t_out, "coeff": torch.from_numpy(gco[:, j0:j1, :].copy())}
+    origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    HaloStencil(st, ["in_field"], nj, h, rank, world, periodic=True)(args, origin, (nig, nj, nk))
+    np.save(os.path.join(outdir, f"out_{rank}.npy"), t_out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_jstrips_periodic(tmp_path, world):
+    """Periodic J strips: two ranks are each other's prev and next (message order matters), one
+    rank copies its own faces (gloo cannot send to itself; RCCL self-sends: scripts/rccl_halo_selftest.py)."""
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, REPO)
+    import stencil_cases as sc
+    from gt4py_amd import gtscript
+
+    port = _free_port()
+    mp.spawn(_worker1d_periodic, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    gin, gco = _global_inputs((False, True))
+    h = 2
+    ref = np.zeros(gco.shape)
+    st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist1dp.hdiff")
+    st(gin.copy(), ref, gco, origin={"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)})
+    got = np.concatenate([np.load(tmp_path / f"out_{r}.npy") for r in range(world)], axis=1)
+    assert np.array_equal(got, ref)
