@@ -207,7 +207,18 @@ def main():
     ap.add_argument("--jchunk", type=int, default=None)
     ap.add_argument("--decomp", default="jstrips", choices=["jstrips", "2d"],
                     help="N>1: J strips (default) or a balanced 2-D process grid (corners exchanged)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: exchange first, then one kernel over the whole strip (no interior/boundary split)")
+    ap.add_argument("--halo-selfcomm", action="store_true",
+                    help="N=1 under torchrun: run the J-strip halo path with the rank as its own periodic "
+                         "neighbour through RCCL (measures the per-rank cost of the exchange + split)")
     args = ap.parse_args()
+
+    # exactly one JSON line on stdout: native libraries (RCCL's version banner, ...) write to fd 1,
+    # so fd 1 is pointed at stderr for the whole run and the result goes to a saved copy of it
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
 
@@ -220,10 +231,12 @@ def main():
     torch.cuda.set_device(local_rank % ndev)
     dev = torch.device("cuda", local_rank % ndev)
     dist = None
-    if world > 1:
+    if world > 1 or args.halo_selfcomm:
         from gt4py_amd.distributed import init_process_group
 
-        # nccl (= RCCL over xGMI) on a real node; GTMI_DIST_BACKEND=gloo rehearses N ranks on one GPU
+        # nccl (= RCCL over xGMI) on a real node; GTMI_DIST_BACKEND=gloo rehearses N ranks on one GPU.
+        # Keep RCCL's version banner off stdout: rank 0 prints exactly one JSON line there.
+        os.environ.setdefault("NCCL_DEBUG", "WARN")
         init_process_group(os.environ.get("GTMI_DIST_BACKEND", "nccl"))
         import torch.distributed as dist
 
@@ -271,11 +284,14 @@ def main():
             origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
         if dec2d is not None:
             # 2-D tile: two-phase (corner-correct) exchange on the halo stream, interior overlapped
-            halo = HaloStencil2D(stencil, ["in_field"], dec2d, rank, (h, h))
+            halo = HaloStencil2D(stencil, ["in_field"], dec2d, rank, (h, h), overlap=not args.no_overlap)
         elif world > 1:
             # J-strip of the global domain: exchange the in_field halo with the neighbours over
             # RCCL while the interior rows compute, then the two boundary strips
-            halo = HaloStencil(stencil, ["in_field"], nj, h, rank, world)
+            halo = HaloStencil(stencil, ["in_field"], nj, h, rank, world, overlap=not args.no_overlap)
+        elif args.halo_selfcomm:
+            halo = HaloStencil(stencil, ["in_field"], nj, h, 0, 1, periodic=True, force_comm=True,
+                               overlap=not args.no_overlap)
     elif sname == "tridiagonal_solver":
         fields = [uniform((ni, nj, nk), lo, hi, (0, 0, 0)) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0))]
         call_args = tuple(fields)
@@ -365,7 +381,7 @@ def main():
             "backend": "gt:mi355x",
             "parallelism": (f"ij-strips{world}" if dec2d is None else f"ij-tiles{dec2d.pi}x{dec2d.pj}")
             if world > 1
-            else "single",
+            else ("single+halo-selfcomm" if args.halo_selfcomm else "single"),
         },
         "roofline": {
             "bound": "hbm",
@@ -383,7 +399,7 @@ def main():
         if cb is not None:
             result["cpu_baseline"] = cb
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

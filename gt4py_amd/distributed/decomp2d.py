@@ -112,6 +112,7 @@ class HaloExchange2D:
             "N": decomp.rank_of(ci, cj + 1) if self.hj else None,
         }
         self._host = None
+        self._copies: Dict[Tuple, Tuple] = {}
         self._bufs: Dict[Tuple, object] = {}
         self._stream = None
 
@@ -155,11 +156,17 @@ class HaloExchange2D:
             total = sum(sizes[d])
             sbuf[d] = self._buffer(("s", phase, d, fields[0].dtype), total, fields[0])
             rbuf[d] = self._buffer(("r", phase, d, fields[0].dtype), total, fields[0])
-            off = 0
-            for t, n in zip(fields, sizes[d]):
-                face = t[faces[d][0][0], faces[d][0][1], :]
-                sbuf[d][off : off + n].view(face.shape).copy_(face)
-                off += n
+        device = (not self._host) and getattr(fields[0], "is_cuda", False)
+        if device:  # one batched launch packs every face of the phase
+            pack, unpack_dev = self._device_copies(fields, phase, faces, dirs, sizes, sbuf, rbuf)
+            pack.run(0)
+        else:
+            for d in dirs:
+                off = 0
+                for t, n in zip(fields, sizes[d]):
+                    face = t[faces[d][0][0], faces[d][0][1], :]
+                    sbuf[d][off : off + n].view(face.shape).copy_(face)
+                    off += n
         # my d-halo receives the neighbour's opposite face. Sends are posted in the opposite
         # order of the receives, so that with two ranks on a periodic axis (W and E are the same
         # peer) the k-th receive from a peer matches that peer's k-th send.
@@ -181,12 +188,40 @@ class HaloExchange2D:
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        if device:
+            for d, buf in unpack:
+                if buf is not rbuf[d]:  # local periodic wrap: my own opposite face
+                    rbuf[d].copy_(buf)
+            unpack_dev.run(1)
+            return
         for d, buf in unpack:
             off = 0
             for t, n in zip(fields, sizes[d]):
                 face = t[faces[d][1][0], faces[d][1][1], :]
                 face.copy_(buf[off : off + n].view(face.shape))
                 off += n
+
+    def _device_copies(self, fields, phase, faces, dirs, sizes, sbuf, rbuf):
+        from gt4py_amd.distributed.halo_copy import BatchedCopy
+
+        key = (phase,) + tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype) for t in fields) + tuple(
+            (sbuf[d].data_ptr(), rbuf[d].data_ptr()) for d in dirs
+        )  # buffers included: a re-allocated message buffer never meets a stale descriptor
+        if key not in self._copies:
+            pack, unpack = [], []
+            for d in dirs:
+                soff = roff = 0
+                for t, n in zip(fields, sizes[d]):
+                    nk = t.shape[2]
+                    (si, sj), (ri, rj) = faces[d]
+                    pack.append((t, (si.start, sj.start, 0), (si.stop - si.start, sj.stop - sj.start, nk),
+                                 sbuf[d][soff : soff + n]))
+                    unpack.append((t, (ri.start, rj.start, 0), (ri.stop - ri.start, rj.stop - rj.start, nk),
+                                   rbuf[d][roff : roff + n]))
+                    soff += n
+                    roff += n
+            self._copies[key] = (BatchedCopy(pack), BatchedCopy(unpack))
+        return self._copies[key]
 
     def exchange(self, fields: Sequence) -> None:
         """Fill the halos (and corners) of ``fields``; must be called by every rank."""

@@ -76,6 +76,8 @@ class JHaloExchange:
         self._bufs: Dict[Tuple, Dict] = {}
         self._pending: List = []
         self._stage_host: Optional[bool] = None
+        self._copies: Dict[Tuple, Tuple] = {}
+        self._pending_device = None
 
     def _global_rank(self, r):
         import torch.distributed as dist
@@ -93,12 +95,33 @@ class JHaloExchange:
             self._bufs[key] = {"send_lo": mk(), "send_hi": mk(), "recv_lo": mk(), "recv_hi": mk()}
         return self._bufs[key]
 
+    def _device_copies(self, fields):
+        """Batched pack/unpack descriptors (one launch each) for this list of device fields."""
+        from gt4py_amd.distributed.halo_copy import BatchedCopy
+
+        key = tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype) for t in fields)
+        if key not in self._copies:
+            h, nj = self.h, self.nj
+            pack, unpack = [], []
+            for t in fields:
+                b = self._buffers(t)
+                ni, _, nk = t.shape
+                if self.next is not None:
+                    pack.append((t, (0, nj, 0), (ni, h, nk), b["send_hi"]))
+                    unpack.append((t, (0, nj + h, 0), (ni, h, nk), b["recv_hi"]))
+                if self.prev is not None:
+                    pack.append((t, (0, h, 0), (ni, h, nk), b["send_lo"]))
+                    unpack.append((t, (0, 0, 0), (ni, h, nk), b["recv_lo"]))
+            self._copies[key] = (BatchedCopy(pack), BatchedCopy(unpack))
+        return self._copies[key]
+
     def start(self, fields: Sequence) -> List:
         """Pack faces and post the sends/receives; returns the pending work handles.
 
         Every send is posted before every receive, sends hi-face first and receives lo-halo
         first: with one peer on both sides (two ranks on a periodic axis, or one rank and
         ``force_comm``) the k-th receive from a peer then matches that peer's k-th send.
+        Device fields are packed by ONE batched kernel launch (``halo_copy.py``).
         """
         import torch.distributed as dist
 
@@ -107,14 +130,19 @@ class JHaloExchange:
             self._stage_host = _backend_name(self.group) == "gloo"
         h, nj = self.h, self.nj
         self._pending = []
+        device = (not self._stage_host) and len(fields) > 0 and getattr(fields[0], "is_cuda", False)
+        if device:
+            pack, _ = self._device_copies(fields)
+            pack.run(0)
         sends, recvs = [], []
         local = lambda peer: peer == self.rank and not self.force_comm  # noqa: E731
         for t in fields:
             b = self._buffers(t)
-            if self.next is not None:
-                b["send_hi"].copy_(t[:, nj : nj + h, :])
-            if self.prev is not None:
-                b["send_lo"].copy_(t[:, h : 2 * h, :])
+            if not device:
+                if self.next is not None:
+                    b["send_hi"].copy_(t[:, nj : nj + h, :])
+                if self.prev is not None:
+                    b["send_lo"].copy_(t[:, h : 2 * h, :])
             if self.next is not None and not local(self.next):
                 sends.append(dist.P2POp(dist.isend, b["send_hi"], self._global_rank(self.next), self.group))
             if self.prev is not None and not local(self.prev):
@@ -130,6 +158,7 @@ class JHaloExchange:
                 else:
                     recvs.append(dist.P2POp(dist.irecv, b["recv_hi"], self._global_rank(self.next), self.group))
             self._pending.append((t, b))
+        self._pending_device = fields if device else None
         ops = sends + recvs
         if not ops:
             return []
@@ -139,6 +168,12 @@ class JHaloExchange:
         """Wait for the transfers and unpack the received faces into the halos."""
         for w in works:
             w.wait()
+        if self._pending_device is not None:
+            _, unpack = self._device_copies(self._pending_device)
+            unpack.run(1)
+            self._pending = []
+            self._pending_device = None
+            return
         h, nj = self.h, self.nj
         for t, b in self._pending:
             if self.prev is not None:
@@ -167,6 +202,7 @@ class HaloStencil:
         self.h = halo
         self.nj = nj_local
         self.overlap = overlap and (world_size > 1 or force_comm) and nj_local > 2 * halo
+        self._stream = None
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
@@ -183,10 +219,29 @@ class HaloStencil:
             self.stencil(**kw, origin=origin, domain=domain, validate_args=False)
             return
         h = self.h
-        works = self.exchange.start(fields)
-        # interior rows [h, nj - h): read rows [0, nj) of the halo'ed fields only
-        self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
-        self.exchange.finish(works)
+        on_gpu = bool(fields) and getattr(fields[0], "is_cuda", False) and _backend_name(self.exchange.group) != "gloo"
+        if on_gpu:
+            # the interior (rows [h, nj-h): reads no halo) is enqueued FIRST on the compute stream,
+            # so the host cost of posting the RCCL work is hidden behind it; packing, transfers
+            # and unpacking run on the halo stream (after the fields' producers), then the two
+            # boundary strips follow on the compute stream.
+            import torch
+
+            dev = fields[0].device
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(device=dev)
+            main = torch.cuda.current_stream(dev)
+            ready = main.record_event()
+            self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
+            self._stream.wait_event(ready)
+            with torch.cuda.stream(self._stream):
+                self.exchange.finish(self.exchange.start(fields))
+            main.wait_stream(self._stream)
+        else:
+            works = self.exchange.start(fields)
+            # interior rows [h, nj - h): read rows [0, nj) of the halo'ed fields only
+            self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
+            self.exchange.finish(works)
         self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
         self.stencil(**kw, origin=self._shifted(origin, nj - h), domain=(ni, h, nk), validate_args=False)
 

@@ -252,3 +252,29 @@ def test_stencil_graph_replay_matches_eager():
         torch.cuda.synchronize()
         assert np.array_equal(got, storage.to_numpy(out_e)), trial
         assert np.array_equal(got, ref), trial
+
+
+def test_batched_halo_copy_roundtrip():
+    """gtmi_halo_copy packs strided boxes of several fields into contiguous buffers and back."""
+    torch = _torch()
+    from gt4py_amd.distributed.halo_copy import BatchedCopy
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    a = torch.rand((37, 29, 7), generator=g, device=dev, dtype=torch.float64)
+    b = torch.as_strided(torch.rand(40 * 33 * 9, generator=g, device=dev, dtype=torch.float32).contiguous(),
+                         (33, 29, 9), (1, 40, 40 * 29))
+    boxes = [(a, (0, 3, 0), (37, 2, 7)), (a, (5, 20, 2), (9, 4, 5)), (b, (1, 0, 0), (32, 29, 9))]
+    bufs = [torch.empty(e[0] * e[1] * e[2], dtype=t.dtype, device=dev) for t, _, e in boxes]
+    BatchedCopy([(t, s, e, buf) for (t, s, e), buf in zip(boxes, bufs)]).run(0)
+    torch.cuda.synchronize()
+    for (t, s, e), buf in zip(boxes, bufs):
+        ref = t[s[0]:s[0] + e[0], s[1]:s[1] + e[1], s[2]:s[2] + e[2]].permute(2, 1, 0).reshape(-1)
+        assert torch.equal(buf, ref)
+    a2, b2 = torch.zeros_like(a), torch.zeros_like(b)
+    BatchedCopy([(t2, s, e, buf) for (t, s, e), buf, t2 in zip(boxes, bufs, (a2, a2, b2))]).run(1)
+    torch.cuda.synchronize()
+    for (t, s, e), t2 in zip(boxes, (a2, a2, b2)):
+        sl = (slice(s[0], s[0] + e[0]), slice(s[1], s[1] + e[1]), slice(s[2], s[2] + e[2]))
+        assert torch.equal(t2[sl], t[sl])
