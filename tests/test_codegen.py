@@ -78,3 +78,17 @@ def test_library_loads_and_describes_itself(name):
     assert lib.last_error() == ""
     with open(HEADER) as fh:
         assert f"#define GTMI_ABI_VERSION {ffi.GTMI_ABI_VERSION}" in fh.read()
+
+
+def test_halo_library_exports_its_header():
+    """The halo pack/unpack library builds for gfx950 and exports exactly include/gtmi_halo.h."""
+    from gt4py_amd.distributed import halo_copy
+
+    path = halo_copy.library_path()
+    hdr = os.path.join(os.path.dirname(HEADER), "gtmi_halo.h")
+    with open(hdr) as f:
+        declared = sorted(set(re.findall(r"^(?:int|const char\*|void)\s+(gtmi_\w+)\s*\(", f.read(), re.M)))
+    assert declared == ["gtmi_halo_abi_version", "gtmi_halo_copy", "gtmi_halo_last_error"]
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(declared) <= exported
