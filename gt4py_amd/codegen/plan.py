@@ -98,8 +98,10 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_pl
             kernels.append(ColumnKernel(list(run)))
             run.clear()
         run_written.clear()
+        run_read_ij.clear()
 
     run_written: Set[str] = set()
+    run_read_ij: Set[str] = set()
     for li, vl in enumerate(st.vertical_loops):
         plane = vl.loop_order == ir.LoopOrder.PARALLEL and (
             _has_horizontal_offsets(vl) or (pointwise_plane and _pointwise_plane_ok(vl))
@@ -129,14 +131,19 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_pl
                             f"offset {acc.offset[:2]} in the same loop"
                         )
             # a column kernel may not consume values at IJ offsets produced earlier in the same run
+            # (RAW across columns), nor overwrite values an earlier loop of the run read at IJ
+            # offsets (WAR across columns): either needs a grid-wide barrier -> new kernel
+            accs = list(_loop_accesses(vl))
             if any(
                 not w and isinstance(a, ir.FieldAccess) and a.name in run_written and (a.offset[0] or a.offset[1])
-                for a, w in _loop_accesses(vl)
-            ):
+                for a, w in accs
+            ) or any(w and a.name in run_read_ij for a, w in accs):
                 flush()
-                run_written.clear()
             run.append(li)
-            run_written.update(a.name for a, w in _loop_accesses(vl) if w)
+            run_written.update(a.name for a, w in accs if w)
+            run_read_ij.update(
+                a.name for a, w in accs if not w and isinstance(a, ir.FieldAccess) and (a.offset[0] or a.offset[1])
+            )
     flush()
 
     # which kernel(s) / loops touch each temporary

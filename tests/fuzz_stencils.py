@@ -1,0 +1,124 @@
+"""Random GTScript program generator for differential testing (gt:mi355x vs the numpy backend).
+
+``generate(seed)`` writes a stencil definition to a module source: three input fields with an
+IJ halo of 2 (plus K slack), two outputs, a few temporaries; statements are random arithmetic
+expression trees over fields/temporaries at random offsets, ternaries, if/else blocks and
+min/max/abs; computations are PARALLEL (IJ offsets), or FORWARD/BACKWARD with K recurrences on
+temporaries. Everything stays within the declared halos so the same inputs are valid for any
+program, and only exactly-rounded operations are used, so results must be bit-identical.
+"""
+
+import random
+
+HALO = 2
+NAMES_IN = ("a", "b", "c")
+
+
+class _Gen:
+    def __init__(self, seed):
+        self.r = random.Random(seed)
+        self.temps = []  # (name, ij_extent_used)
+        self.lines = []
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if allow_temps and self.temps and r.random() < 0.4:
+            t = r.choice(self.temps)
+            # temporaries at IJ offsets only from the outputs (extent stays within the halo of 2)
+            di, dj = (r.randint(-1, 1), r.randint(-1, 1)) if (kmode == "par" and allow_temps == "offsets") else (0, 0)
+            return f"{t}[{di}, {dj}, 0]"
+        if r.random() < 0.15:
+            return repr(round(r.uniform(-3, 3), 3))
+        f = r.choice(NAMES_IN)
+        di, dj = r.randint(-1, 1), r.randint(-1, 1)
+        dk = r.choice((0, 0, 0, 1, -1)) if kmode == "par" else 0
+        return f"{f}[{di}, {dj}, {dk}]"
+
+    def expr(self, depth, allow_temps, kmode):
+        r = self.r
+        if depth == 0 or r.random() < 0.25:
+            return self.leaf(allow_temps, kmode)
+        kind = r.random()
+        x = self.expr(depth - 1, allow_temps, kmode)
+        y = self.expr(depth - 1, allow_temps, kmode)
+        if kind < 0.55:
+            op = r.choice(("+", "-", "*"))
+            return f"({x} {op} {y})"
+        if kind < 0.65:
+            return f"({x} / (abs({y}) + 1.5))"
+        if kind < 0.8:
+            fn = r.choice(("min", "max"))
+            return f"{fn}({x}, {y})"
+        if kind < 0.9:
+            z = self.expr(depth - 1, allow_temps, kmode)
+            return f"({x} if {y} > {z} else {z})"
+        return f"abs({x})"
+
+
+def generate(seed):
+    """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
+    cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering."""
+    v2 = seed >= 1000
+    g = _Gen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    L = []
+    L.append(f"def {name}(a: Field[np.float64], b: Field[np.float64], c: Field[np.float64], "
+             f"out1: Field[np.float64], out2: Field[np.float64], *, s: float):")
+    n_comp = r.randint(1, 3)
+    used_out = set()
+    for ci in range(n_comp):
+        order = r.choice(("PARALLEL", "PARALLEL", "FORWARD", "BACKWARD"))
+        kmode = "par" if order == "PARALLEL" else "seq"
+        if order == "PARALLEL":
+            L.append("    with computation(PARALLEL), interval(1, -1):")
+            nst = r.randint(1, 4)
+            for si in range(nst):
+                t = f"t{ci}_{si}"
+                L.append(f"        {t} = {g.expr(3, True, kmode)}")
+                g.temps.append(t)
+            if r.random() < 0.5:
+                cond = g.expr(1, "offsets", kmode)
+                L.append(f"        if {cond} > s:")
+                L.append(f"            out1 = {g.expr(2, 'offsets', kmode)}")
+                L.append("        else:")
+                L.append(f"            out1 = {g.expr(2, 'offsets', kmode)} * s")
+            else:
+                L.append(f"        out1 = {g.expr(3, 'offsets', kmode)}")
+            used_out.add("out1")
+            if v2 and r.random() < 0.6:
+                ib = r.choice(("region[I[0] : I[0] + 2, :]", "region[:, J[-1] - 1 : J[-1]]",
+                               "region[I[0] : I[0] + 3, J[0] : J[0] + 2]", "region[I[-1] - 2 : I[-1], :]"))
+                L.append(f"        with horizontal({ib}):")
+                L.append(f"            out1 = {g.expr(2, 'offsets', kmode)} + out1")
+            if v2:
+                g.prev_temps = list(g.temps)  # readable (at IJ offsets) by a later sequential sweep
+            g.temps = []  # temporaries are local to the computation
+        else:
+            first, rest = ("interval(0, 1)", "interval(1, None)") if order == "FORWARD" else (
+                "interval(-1, None)", "interval(0, -1)")
+            dk = -1 if order == "FORWARD" else 1
+            L.append(f"    with computation({order}):")
+            L.append(f"        with {first}:")
+            L.append(f"            acc = {g.expr(2, False, kmode)}")
+            L.append("            out2 = acc")
+            L.append(f"        with {rest}:")
+            L.append(f"            acc = acc[0, 0, {dk}] * 0.5 + {g.expr(2, False, kmode)}")
+            L.append(f"            out2 = acc - out2[0, 0, {dk}] * 0.25")
+            used_out.add("out2")
+            if v2 and r.random() < 0.6:
+                # a temporary produced and read at IJ offsets inside one sweep (staged lowering),
+                # optionally mixed with a PARALLEL computation's temporary at an offset
+                extra = ""
+                if getattr(g, "prev_temps", None):  # at an offset: extent 1 (its fields) + 1
+                    extra = f" + {r.choice(g.prev_temps)}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0]"
+                # a PARALLEL temporary is only defined on interval(1, -1): reading it elsewhere reads
+                # uninitialised temporary storage (undefined in GTScript), so stay inside
+                ivl = "interval(1, -1)" if extra else "interval(...)"
+                L.append(f"    with computation({order}), {ivl}:")
+                L.append(f"        u = {r.choice(NAMES_IN)}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0] * 0.5 + 0.25")
+                L.append(f"        out2 = out2 + 0.5 * (u[1, 0, 0] - u[0, -1, 0]){extra}")
+    if not used_out:
+        L.append("    with computation(PARALLEL), interval(...):")
+        L.append("        out1 = a")
+    return "\n".join(L) + "\n", name
