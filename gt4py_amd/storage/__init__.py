@@ -151,17 +151,25 @@ def full(shape, fill_value, dtype=np.float64, *, backend, aligned_index=None, di
     return arr
 
 
-def from_array(data, dtype=None, *, backend, aligned_index=None, dimensions=None):
-    """Allocate with the backend's layout and copy ``data`` (numpy / torch / array-like) in."""
+def from_array(data, dtype=np.float64, *, backend, aligned_index=None, dimensions=None):
+    """Allocate with the backend's layout and copy ``data`` (numpy / torch / array-like) in.
+
+    As ``storage/cartesian/interface.py:263-327``: ``dtype`` defaults to float64 (``None`` keeps
+    the data's dtype); a subarray dtype ``(base, dims)`` takes its data dimensions from the
+    trailing axes of ``data``, which must match ``dims``.
+    """
     if hasattr(data, "detach") and hasattr(data, "cpu"):
         host = data.detach().cpu().numpy()
     else:
         host = np.asarray(data)
-    if dtype is None:
-        dtype = host.dtype
+    dtype = np.dtype(host.dtype if dtype is None else dtype)
     shape = host.shape
+    if dtype.shape:
+        if tuple(shape[-dtype.ndim:]) != tuple(dtype.shape):
+            raise ValueError(f"Incompatible data shape {shape} with dtype of shape {dtype.shape}.")
+        shape = shape[: -dtype.ndim]
     arr = empty(shape, dtype, backend=backend, aligned_index=aligned_index, dimensions=dimensions)
-    _copy_in(arr, host.astype(np.dtype(dtype), copy=False))
+    _copy_in(arr, host.astype(dtype.base, copy=False))
     return arr
 
 

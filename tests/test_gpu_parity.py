@@ -46,7 +46,7 @@ def run_case_on_gpu(case):
             continue
         fi = stencil.field_info.get(k)
         if fi is None:  # unused by the stencil: any layout
-            dev[k] = storage.from_array(v, backend=BACKEND, aligned_index=_origin_of(case, k, v.ndim))
+            dev[k] = storage.from_array(v, None, backend=BACKEND, aligned_index=_origin_of(case, k, v.ndim))
             continue
         axes = tuple(fi.axes)
         dims = axes + tuple(str(d) for d in range(len(fi.data_dims)))
@@ -58,7 +58,7 @@ def run_case_on_gpu(case):
         else:
             org = tuple(o["IJK".index(a)] for a in axes)
         dev[k] = storage.from_array(
-            v, backend=BACKEND, aligned_index=org + (0,) * len(fi.data_dims), dimensions=dims
+            v, None, backend=BACKEND, aligned_index=org + (0,) * len(fi.data_dims), dimensions=dims
         )
     kw = {}
     if case.origin is not None:
@@ -88,7 +88,7 @@ def _alloc_fill(shape, dtype, rng, lo, hi, origin):
     from gt4py_amd import storage
 
     host = rng.uniform(lo, hi, size=shape).astype(dtype)
-    return host, storage.from_array(host, backend=BACKEND, aligned_index=origin)
+    return host, storage.from_array(host, None, backend=BACKEND, aligned_index=origin)
 
 
 @pytest.mark.parametrize("dtype,ni,nj,nk", [(np.float64, 2048, 2048, 160), (np.float32, 1024, 1024, 64)])
