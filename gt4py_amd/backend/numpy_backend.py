@@ -145,7 +145,8 @@ class NumpyExecutor:
             fields[t.name] = _Arr(arr, (ilo, jlo, 0), mask)
         self.fields, self.scalars, self.domain = fields, scalars, (ni, nj, nk)
         self.api = {p.name for p in st.field_params()}
-        with np.errstate(divide="ignore", over="ignore", under="ignore", invalid="ignore"):
+        errs = "ignore" if getattr(self, "ignore_errstate", True) else "warn"
+        with np.errstate(divide=errs, over=errs, under="ignore", invalid=errs):
             for li, vl in enumerate(st.vertical_loops):
                 for si, sec in enumerate(vl.sections):
                     k0, k1 = sec.interval.resolve(nk)
@@ -379,6 +380,8 @@ class NumpyBackend(BaseBackend):
     options = {
         "oir_pipeline": {"versioning": True, "type": object},
         "verbose": {"versioning": False, "type": bool},
+        # numpy_backend.py:36,43: False runs the computation under numpy's default error state
+        "ignore_np_errstate": {"versioning": True, "type": bool},
     }
     _layout = layout_maker_factory((0, 1, 2))
     storage_info = {
@@ -391,6 +394,7 @@ class NumpyBackend(BaseBackend):
 
     def make_run_impl(self):
         executor = NumpyExecutor(self.builder.analysis)
+        executor.ignore_errstate = bool(self.builder.options.backend_opts.get("ignore_np_errstate", True))
 
         def run_impl(domain, origin, exec_info, kwargs):
             executor.run(domain, origin, kwargs)

@@ -396,6 +396,56 @@ def compute_extents(stencil: ir.Stencil) -> ExtentInfo:
     return ExtentInfo(fields, blocks)
 
 
+def _accesses_with_region(stmts, in_region=False):
+    """(access, is_write, inside a horizontal region) in :func:`iter_accesses` order."""
+    for s in stmts:
+        if isinstance(s, ir.HorizontalRegion):
+            yield from _accesses_with_region(s.body, True)
+        elif isinstance(s, (ir.If, ir.While)):
+            for acc, w in iter_accesses([type(s)(s.cond, [], []) if isinstance(s, ir.If) else type(s)(s.cond, [])]):
+                yield acc, w, in_region
+            yield from _accesses_with_region(s.body, in_region)
+            if isinstance(s, ir.If):
+                yield from _accesses_with_region(s.orelse, in_region)
+        else:
+            for acc, w in iter_accesses([s]):
+                yield acc, w, in_region
+
+
+def compute_signed_extents(stencil: ir.Stencil) -> Dict[str, Extent]:
+    """Per-field extents as signed offset ranges ``((i_min, i_max), (j_min, j_max))``, the
+    non-centered extents the reference reports in ``FieldInfo.boundary``
+    (``oir_optimizations/utils.py:250-315``: a read at ``he + offset`` is NOT widened to include
+    offset 0, so a field read only at ``[1, 0, 0]`` gets the boundary ``(-1, 1)`` in I and may be
+    called with origin -1; accesses inside horizontal regions are widened to 0). Code generation
+    keeps using the centered halo sizes of :func:`compute_extents`."""
+    zero = ((0, 0), (0, 0))
+
+    def union(a, b):
+        return ((min(a[0][0], b[0][0]), max(a[0][1], b[0][1])), (min(a[1][0], b[1][0]), max(a[1][1], b[1][1])))
+
+    fields: Dict[str, Extent] = {}
+    for vl in reversed(stencil.vertical_loops):
+        for sec in reversed(vl.sections):
+            for stmt in reversed(sec.body):
+                accesses = list(_accesses_with_region([stmt]))
+                he = zero
+                for acc, is_write, _ in accesses:
+                    if is_write:
+                        he = union(he, fields.setdefault(acc.name, zero))
+                for acc, _, in_region in accesses:
+                    if not isinstance(acc, ir.FieldAccess):
+                        continue
+                    di, dj = acc.offset[0], acc.offset[1]
+                    ext = ((he[0][0] + di, he[0][1] + di), (he[1][0] + dj, he[1][1] + dj))
+                    if in_region:
+                        ext = union(ext, zero)
+                    fields[acc.name] = union(fields[acc.name], ext) if acc.name in fields else ext
+    for p in stencil.params:
+        fields.setdefault(p.name, zero)
+    return fields
+
+
 # --------------------------------------------------------------------------------------
 # K boundary and minimal K size
 # --------------------------------------------------------------------------------------
@@ -481,7 +531,13 @@ class StencilAnalysis:
     k_boundary: Dict[str, Tuple[int, int]]
     min_k_size: int
 
+    signed_extents: Optional[Dict[str, Extent]] = None
+
     def boundary(self, name: str):
+        """``FieldInfo.boundary``: (-min, max) of the signed I/J extents, the K boundary."""
+        if self.signed_extents is not None and name in self.signed_extents:
+            (a, b), (c, d) = self.signed_extents[name]
+            return ((-a, b), (-c, d), self.k_boundary.get(name, (0, 0)))
         e = self.extents.fields.get(name, ZERO_EXTENT)
         return (e[0], e[1], self.k_boundary.get(name, (0, 0)))
 
@@ -498,4 +554,4 @@ def run_pipeline(stencil: ir.Stencil) -> StencilAnalysis:
     access = compute_access_kinds(stencil)
     kb = compute_k_boundary(stencil)
     min_k = compute_min_k_size(stencil)
-    return StencilAnalysis(stencil, access, extents, kb, min_k)
+    return StencilAnalysis(stencil, access, extents, kb, min_k, compute_signed_extents(stencil))

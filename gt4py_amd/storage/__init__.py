@@ -42,28 +42,39 @@ def _error_on_invalid_preset(backend):
         raise RuntimeError(f"Storage preset '{backend}' is not registered.")
 
 
-def _normalize_spec(aligned_index, shape, dtype, dimensions):
-    """Validate the spec; a subarray dtype appends its shape as trailing data dimensions
-    (aligned index 0 there), as ``storage/cartesian/utils.py:84-170`` does."""
-    if not isinstance(shape, (tuple, list)) or not all(isinstance(s, numbers.Integral) for s in shape):
-        raise TypeError("shape must be a sequence of integers")
-    shape = tuple(int(s) for s in shape)
+def normalize_storage_spec(aligned_index, shape, dtype, dimensions):
+    """Homogeneous ``(aligned_index, shape, dtype, dimensions)``; the checks, their order and the
+    error types of ``storage/cartesian/utils.py:84-167``. A subarray dtype appends its shape as
+    trailing data dimensions (aligned index 0 there)."""
+    if shape is None or isinstance(shape, (str, bytes)) or not isinstance(shape, Sequence):
+        raise TypeError("shape must be an iterable of ints.")
     if dimensions is None:
         dimensions = ("I", "J", "K")[: min(3, len(shape))] + tuple(str(d) for d in range(len(shape) - 3))
-    dimensions = tuple(str(getattr(d, "__gt_axis_name__", d)) for d in dimensions)
-    if not all(d.isdigit() or d in ("I", "J", "K") for d in dimensions):
+    dimensions = tuple(getattr(d, "__gt_axis_name__", d) for d in dimensions)
+    if not all(isinstance(d, str) and (d.isdigit() or d in ("I", "J", "K")) for d in dimensions):
         raise ValueError(f"Invalid dimensions definition: '{dimensions}'")
-    if len(dimensions) != len(shape):
-        raise ValueError(f"dimensions {dimensions} do not match shape {shape}")
-    if any(s <= 0 for s in shape):
+    if not all(isinstance(x, numbers.Integral) for x in shape):
+        raise TypeError("shape must be an iterable of ints.")
+    if len(shape) != len(dimensions):
+        raise ValueError(
+            f"Dimensions ({dimensions}) and shape ({tuple(shape)}) have non-matching sizes: "
+            f"len(shape)={len(shape)} must equal len(dimensions)={len(dimensions)}."
+        )
+    shape = tuple(int(x) for x in shape)
+    if any(x <= 0 for x in shape):
         raise ValueError(f"shape ({shape}) contains non-positive value.")
     if aligned_index is None:
         aligned_index = (0,) * len(shape)
-    aligned_index = tuple(int(a) for a in aligned_index)
+    if (isinstance(aligned_index, (str, bytes)) or not isinstance(aligned_index, Sequence)
+            or not all(isinstance(a, numbers.Integral) for a in aligned_index)):
+        raise TypeError("aligned_index must be an iterable of ints.")
     if len(aligned_index) != len(shape):
-        raise ValueError("aligned_index must have one entry per dimension")
+        raise ValueError(
+            f"Shape ({shape}) and aligned_index ({tuple(aligned_index)}) have non-matching sizes."
+        )
+    aligned_index = tuple(int(a) for a in aligned_index)
     if any(a < 0 for a in aligned_index):
-        raise ValueError("aligned_index must be non-negative")
+        raise ValueError(f"aligned_index ({aligned_index}) contains negative value.")
     dtype = np.dtype(dtype)
     if dtype.shape:
         sub = tuple(dtype.shape)
@@ -71,27 +82,66 @@ def _normalize_spec(aligned_index, shape, dtype, dimensions):
         aligned_index = aligned_index + (0,) * len(sub)
         dimensions = dimensions + tuple(str(d) for d in range(len(sub)))
         dtype = dtype.base
-    return aligned_index, shape, dtype, dimensions
+    return aligned_index, shape, dtype, tuple(str(d) for d in dimensions)
+
+
+_normalize_spec = normalize_storage_spec
 
 
 def _allocation_plan(shape, layout_map, itemsize, alignment_bytes, aligned_index):
-    """Padded strides (elements) and element offset of the aligned index (int64-safe)."""
+    """Padded element strides, element offset of the first element (so that ``aligned_index``
+    lands on an ``alignment_bytes`` boundary when the buffer base does), total elements.
+    64-bit Python ints throughout."""
     if alignment_bytes % itemsize:
         raise ValueError("alignment must be a multiple of the item size")
     align_el = max(1, alignment_bytes // itemsize)
     ndim = len(shape)
     if ndim == 0:
         return (), 0, 1, align_el
-    order = sorted(range(ndim), key=lambda d: layout_map[d])  # slowest .. fastest
-    fastest = order[-1]
+    fastest = max(range(ndim), key=lambda d: layout_map[d])
     padded = list(shape)
     padded[fastest] = int(math.ceil(max(shape[fastest], 1) / align_el) * align_el)
     strides = make_strides(padded, layout_map)
-    # shift so that aligned_index lands on an aligned address
-    ai_off = sum(a * s for a, s in zip(aligned_index, strides))
+    ai_off = sum(a * st for a, st in zip(aligned_index, strides))
     shift = (-ai_off) % align_el
-    total = shift + sum((s - 1) * st for s, st in zip(padded, strides)) + 1 if all(padded) else shift + 1
+    total = shift + sum((n - 1) * st for n, st in zip(padded, strides)) + 1
     return tuple(strides), shift, total, align_el
+
+
+def allocate_cpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
+    """``(raw byte buffer, ndarray view)``: ``layout_map`` orders the strides (highest rank
+    contiguous), the contiguous dimension is padded to the alignment and ``aligned_index`` sits on
+    an ``alignment_bytes`` boundary (``storage/cartesian/utils.py:232-248``)."""
+    dtype = np.dtype(dtype)
+    shape = tuple(int(x) for x in shape)
+    aligned_index = tuple(aligned_index) if aligned_index is not None else (0,) * len(shape)
+    strides, shift, total, _ = _allocation_plan(shape, layout_map, dtype.itemsize, alignment_bytes, aligned_index)
+    raw = np.empty(total * dtype.itemsize + alignment_bytes, dtype=np.uint8)
+    base = (-raw.ctypes.data) % alignment_bytes
+    flat = raw[base : base + total * dtype.itemsize].view(dtype)
+    arr = np.lib.stride_tricks.as_strided(
+        flat[shift:], shape=shape, strides=tuple(st * dtype.itemsize for st in strides)
+    )
+    return raw, arr
+
+
+def allocate_gpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
+    """``(flat device buffer, strided tensor view)`` on the current ROCm device, same layout rules
+    as :func:`allocate_cpu` (the reference's CuPy ``allocate_gpu``, ``utils.py:251-316``)."""
+    import torch
+
+    from gt4py_amd.runtime import device as dev
+
+    dtype = np.dtype(dtype)
+    shape = tuple(int(x) for x in shape)
+    aligned_index = tuple(aligned_index) if aligned_index is not None else (0,) * len(shape)
+    strides, shift, total, align_el = _allocation_plan(
+        shape, layout_map, dtype.itemsize, alignment_bytes, aligned_index
+    )
+    buf = torch.empty(int(total + align_el), dtype=torch_dtype(dtype), device=dev.current_device())
+    base = ((-buf.data_ptr()) % alignment_bytes) // dtype.itemsize
+    arr = torch.as_strided(buf, size=shape, stride=strides, storage_offset=int(base + shift))
+    return buf, arr
 
 
 def _device_of(info: LayoutInfo) -> str:
@@ -109,27 +159,10 @@ def empty(
     """Allocate uninitialized storage with the backend's optimal layout and alignment."""
     _error_on_invalid_preset(backend)
     info = REGISTRY[backend]
-    aligned_index, shape, dtype, dimensions = _normalize_spec(aligned_index, shape, dtype, dimensions)
+    aligned_index, shape, dtype, dimensions = normalize_storage_spec(aligned_index, shape, dtype, dimensions)
     layout_map = info["layout_map"](dimensions)
-    strides, shift, total, _ = _allocation_plan(
-        shape, layout_map, dtype.itemsize, info["alignment"] * dtype.itemsize, aligned_index
-    )
-    if _device_of(info) == "gpu":
-        import torch
-
-        from gt4py_amd.runtime import device as dev
-
-        tdtype = torch_dtype(dtype)
-        buf = torch.empty(int(total), dtype=tdtype, device=dev.current_device())
-        arr = torch.as_strided(buf, size=shape, stride=strides, storage_offset=int(shift))
-    else:
-        nbytes = int(total) * dtype.itemsize
-        raw = np.empty(nbytes + 256, dtype=np.uint8)
-        base_off = (-raw.ctypes.data) % 256
-        flat = raw[base_off : base_off + nbytes].view(dtype)
-        arr = np.lib.stride_tricks.as_strided(
-            flat[shift:], shape=shape, strides=tuple(s * dtype.itemsize for s in strides)
-        )
+    alloc = allocate_gpu if _device_of(info) == "gpu" else allocate_cpu
+    _, arr = alloc(shape, layout_map, dtype, info["alignment"] * dtype.itemsize, aligned_index)
     return arr
 
 
@@ -186,7 +219,7 @@ def _copy_in(arr, host: np.ndarray):
     else:
         import torch
 
-        arr.copy_(torch.from_numpy(np.ascontiguousarray(host)))
+        arr.copy_(torch.from_numpy(np.array(host, order="C")))  # keeps 0-d shapes
 
 
 def to_numpy(arr) -> np.ndarray:
@@ -198,6 +231,9 @@ def to_numpy(arr) -> np.ndarray:
     return np.asarray(arr)
 
 
+cpu_copy = to_numpy  # storage/cartesian/utils.py:170-175
+
+
 _TORCH_DTYPES: Dict[np.dtype, Any] = {}
 
 
@@ -207,6 +243,11 @@ def torch_dtype(dtype):
     dtype = np.dtype(dtype)
     table = {
         np.dtype(np.bool_): torch.bool,
+        np.dtype(np.uint8): torch.uint8,
+        np.dtype(np.uint16): torch.uint16,
+        np.dtype(np.uint32): torch.uint32,
+        np.dtype(np.uint64): torch.uint64,
+        np.dtype(np.float16): torch.float16,
         np.dtype(np.int8): torch.int8,
         np.dtype(np.int16): torch.int16,
         np.dtype(np.int32): torch.int32,
@@ -225,6 +266,11 @@ def numpy_dtype_of(arr) -> np.dtype:
 
     table = {
         torch.bool: np.bool_,
+        torch.uint8: np.uint8,
+        torch.uint16: np.uint16,
+        torch.uint32: np.uint32,
+        torch.uint64: np.uint64,
+        torch.float16: np.float16,
         torch.int8: np.int8,
         torch.int16: np.int16,
         torch.int32: np.int32,
@@ -271,6 +317,10 @@ __all__ = [
     "full",
     "from_array",
     "to_numpy",
+    "cpu_copy",
+    "normalize_storage_spec",
+    "allocate_cpu",
+    "allocate_gpu",
     "array_info",
     "layout_maker_factory",
     "layout_checker_factory",
