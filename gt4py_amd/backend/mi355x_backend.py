@@ -86,6 +86,7 @@ class Mi355xBackend(BaseBackend):
         "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow)"},
         "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},
         "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},
+        "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

@@ -80,7 +80,8 @@ class VInit(ir.Stmt):
 
 
 class PlaneGen:
-    def __init__(self, analysis: StencilAnalysis, plan: KernelPlan, kernel: PlaneKernel, slots, kid: int, opts):
+    def __init__(self, analysis: StencilAnalysis, plan: KernelPlan, kernel: PlaneKernel, slots, kid: int, opts,
+                 mirror: bool = False):
         self.a = analysis
         self.st = analysis.stencil
         self.plan = plan
@@ -100,9 +101,14 @@ class PlaneGen:
         self.current: Dict[str, Val] = {}
         self.api = {p.name for p in self.st.field_params()}
         self.scratch = set(plan.scratch)
+        # mirror=True generates the same section streamed in -J (the rows of a chunk visited
+        # top-down): J offsets are negated, J extents swapped, and local row u is row jb + jce - 1 - u
+        self.mirror = mirror
+        self.body = ir.map_expr(self.sec.body, _negate_dj) if mirror else self.sec.body
         self.stage_ext = []
         for ti in range(len(self.sec.body)):
-            self.stage_ext.append(analysis.extents.blocks[(kernel.loop, kernel.section, ti)])
+            (ilo, ihi), (jlo, jhi) = analysis.extents.blocks[(kernel.loop, kernel.section, ti)]
+            self.stage_ext.append(((ilo, ihi), (jhi, jlo) if mirror else (jlo, jhi)))
 
     # -------------------------------------------------------------- value bookkeeping
     def _new_val(self, name, dtype, kind, **kw) -> Val:
@@ -143,7 +149,7 @@ class PlaneGen:
     # -------------------------------------------------------------- SSA construction
     def build(self):
         self.stage_code = []
-        for ti, stmt in enumerate(self.sec.body):
+        for ti, stmt in enumerate(self.body):
             lead = self.stage_ext[ti][1][1]
             needed_lo = self.stage_ext[ti][1][0]
             out: List[ir.Stmt] = []
@@ -281,14 +287,38 @@ class PlaneGen:
             vec = max(1, min(4, 16 // max(sizes))) if sizes else 1
         if vec > 1:
             variants.append(vec)
+        mirrored = None
+        if self._mirror_pays():
+            mirrored = PlaneGen(self.a, self.plan, self.kernel, self.slots, self.kid, self.opts, mirror=True).build()
         srcs = []
         launches = {}
         for V in variants:
             self.geometry(V)
-            src, launch = self._render_variant(V)
+            if mirrored is not None:
+                mirrored.geometry(V)
+                assert (mirrored.h_lo, mirrored.w_out) == (self.h_lo, self.w_out)
+            src, launch = self._render_variant(V, mirrored)
             srcs.append(src)
             launches[V] = launch
         return "\n\n".join(srcs), self._render_host(launches)
+
+    def _mirror_pays(self) -> bool:
+        """Stream odd J chunks top-down (option ``jmirror``, default on).
+
+        Two chunks that meet at a boundary then read the rows they share (the J halo of the
+        section, ``needed_lo + lead`` rows) at the same time -- both at the start or both at the
+        end of their sweep -- so the second read hits the XCD's L2 instead of HBM. Chunks of one
+        level are consecutive work items on one XCD (XCD-aware order), i.e. they run together.
+        """
+        if not int(self.opts.get("jmirror", 1)) or self.mirror:
+            return False
+        if any(n in self.scratch for n in self.current):
+            return False  # scratch stores extend into the J halo of the edge chunks
+        return any(isinstance(n, ir.FieldAccess) and n.offset[1] != 0 for n in ir.walk(self.sec.body))
+
+    def _row(self, local: str) -> str:
+        """Grid row of local row ``local`` of the chunk (``t + lead``)."""
+        return f"(jb + jce - 1 - ({local}))" if self.mirror else f"(jb + ({local}))"
 
     def _used_slots(self):
         used, written = [], set()
@@ -302,7 +332,7 @@ class PlaneGen:
                     used.append(self.slots[name])
         return used, written
 
-    def _render_variant(self, V: int) -> Tuple[str, dict]:
+    def _render_variant(self, V: int, mirrored: Optional["PlaneGen"] = None) -> Tuple[str, dict]:
         k = self.kid
         P = int(self.opts.get("prefetch", 4 if V <= 2 else 2))
         used_slots, written_slots = self._used_slots()
@@ -370,6 +400,22 @@ class PlaneGen:
                 B.append(f"const int64_t li_{c} = (int64_t)gtmi::clampi(pos, p.ilo_{c}, p.ihi_{c}) * p.sI_{c};")
             else:
                 B.append(f"const bool vok_{c} = (pos >= p.ilo_{c}) && (pos + {V - 1} <= p.ihi_{c});")
+        if mirrored is None:
+            B += self._render_body(V, P)
+        else:  # wave-uniform branch: odd chunks stream top-down
+            B.append("if ((chunk & 1) == 0) {")
+            B += ["    " + x for x in self._render_body(V, P)]
+            B.append("} else {")
+            B += ["    " + x for x in mirrored._render_body(V, P)]
+            B.append("}")
+        L += ["    " + x for x in B]
+        L.append("}")
+        geo = {"w_out": self.w_out, "V": V, "kname": kname, "used": used_slots}
+        return "\n".join(L), geo
+
+    def _render_body(self, V: int, P: int) -> List[str]:
+        """Register rings, prefetch and the row loop of one J direction."""
+        B = []
         # rings (+ per-element registers)
         for v in self.vals:
             if v.kind == "undef":
@@ -429,7 +475,7 @@ class PlaneGen:
             first = -(v.needed_lo + v.lead)
             for pp in range(P):
                 B.append(f"if ({self.t_start + pp} >= {first} && {self.t_start + pp} < jce)")
-                B += ["    " + x for x in emit_load(v, f"jb + ({self.t_start + pp}) + ({v.lead})",
+                B += ["    " + x for x in emit_load(v, self._row(f"({self.t_start + pp}) + ({v.lead})"),
                                                    [f"pf{pp}_{v.c}_{e}" for e in range(V)])]
         B.append(f"for (int t = {self.t_start}; t < jce; ++t) {{")
         S = []
@@ -437,7 +483,7 @@ class PlaneGen:
             first = -(v.needed_lo + v.lead)
             if P == 0:
                 S.append(f"if (t >= {first})")
-                S += ["    " + x for x in emit_load(v, f"jb + t + ({v.lead})", [f"{v.c}_0_{e}" for e in range(V)])]
+                S += ["    " + x for x in emit_load(v, self._row(f"t + ({v.lead})"), [f"{v.c}_0_{e}" for e in range(V)])]
             else:
                 for e in range(V):
                     S.append(f"{v.c}_0_{e} = pf0_{v.c}_{e};")
@@ -445,7 +491,7 @@ class PlaneGen:
                     for e in range(V):
                         S.append(f"pf{pp}_{v.c}_{e} = pf{pp + 1}_{v.c}_{e};")
                 S.append(f"if (t + {P} >= {first} && t + {P} < jce)")
-                S += ["    " + x for x in emit_load(v, f"jb + t + {P} + ({v.lead})",
+                S += ["    " + x for x in emit_load(v, self._row(f"t + {P} + ({v.lead})"),
                                                    [f"pf{P - 1}_{v.c}_{e}" for e in range(V)])]
         for ti, code in enumerate(self.stage_code):
             lead = self.stage_ext[ti][1][1]
@@ -461,10 +507,7 @@ class PlaneGen:
                     S.append(f"{v.c}_{a}_{e} = {v.c}_{a - 1}_{e};")
         B += ["    " + x for x in S]
         B.append("}")
-        L += ["    " + x for x in B]
-        L.append("}")
-        geo = {"w_out": self.w_out, "V": V, "kname": kname, "used": used_slots}
-        return "\n".join(L), geo
+        return B
 
     def _render_stores(self) -> List[str]:
         V = self.V
@@ -473,7 +516,7 @@ class PlaneGen:
             if not self._mem_backed(name):
                 continue
             c = cname(name)
-            row = f"jb + t + ({v.lead})"
+            row = self._row(f"t + ({v.lead})")
             if name in self.scratch:
                 (eilo, eihi), (ejlo, ejhi) = self.plan.scratch_extent[name]
                 rcond = (
@@ -624,7 +667,7 @@ class PlaneGen:
 
     def _axis_index(self, lead, e):
         def ax(axis):
-            return [f"i_{e}", f"(jb + t + ({lead}))", "kk"][axis]
+            return [f"i_{e}", self._row(f"t + ({lead})"), "kk"][axis]
 
         return ax
 
@@ -653,13 +696,19 @@ class PlaneGen:
             out.append("}")
             return out
         if isinstance(s, ir.HorizontalRegion):
-            cond = region_condition(s.masks, f"i_{e}", f"(jb + t + ({lead}))", "p.ni", "p.nj")
+            cond = region_condition(s.masks, f"i_{e}", self._row(f"t + ({lead})"), "p.ni", "p.nj")
             out = [f"if ({cond}) {{"]
             for x in s.body:
                 out += ["    " + y for y in self._stmt(x, rend, e, lead)]
             out.append("}")
             return out
         raise TypeError(type(s))
+
+
+def _negate_dj(x):
+    if isinstance(x, ir.FieldAccess) and x.offset[1]:
+        return dataclasses.replace(x, offset=(x.offset[0], -x.offset[1], x.offset[2]))
+    return x
 
 
 def _vrefs_in(node) -> List[VRef]:
