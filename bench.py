@@ -184,7 +184,7 @@ def cpu_baseline(cfg_name, budget_s=10.0):
         fn()
         reps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 200:
+        if el >= budget_s or reps >= 5000:
             break
     cells = ni * nj * nk_s * reps
     return {

@@ -266,6 +266,8 @@ class PlaneGen:
         """Non-temporal loads for streams read once (no IJ offsets), if enabled."""
         if not self.opts.get("nt_load", 1):
             return False
+        if int(self.opts.get("nt_load", 1)) == 2:  # experiment: every load non-temporal
+            return True
         return v.needed_ilo == 0 and v.needed_ihi == 0 and v.depth == 1
 
     def _lane_range(self, v: Val) -> Tuple[int, int]:

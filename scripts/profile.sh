@@ -9,11 +9,14 @@ TAG=${TAG:-r01}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 for cfg in ${CONFIGS:-hdiff}; do
-  echo "== $cfg: bench"
-  timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_$cfg.json 2> $OUT/bench_$cfg.err || exit $?
+  # the bench line and the kernel-trace stats come from the SAME run, so rocprof's average kernel
+  # duration and the bench's HIP-event kernel time describe the same launches
+  cpu=--no-cpu-baseline
+  [ "$cfg" = hdiff ] && cpu=
+  echo "== $cfg: bench under kernel trace"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python3 bench.py --config $cfg --steps 20 --warmup 3 $cpu > $OUT/kt_$cfg.log 2>&1 || exit $?
+  grep '^{"metric"' $OUT/kt_$cfg.log > $OUT/bench_$cfg.json || exit $?
   cat $OUT/bench_$cfg.json
-  echo "== $cfg: kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline > $OUT/kt_$cfg.log 2>&1 || exit $?
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg: pmc $c"
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${cfg}_$c -o pmc -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_${cfg}_$c.log 2>&1 || exit $?

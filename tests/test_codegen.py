@@ -59,6 +59,22 @@ def _lib_path(stencil):
     raise AssertionError("no compiled library attached")
 
 
+def test_jmirror_variants_build():
+    """Odd J chunks of a plane kernel with J offsets stream top-down unless jmirror=0 (also builds
+    the libraries tests/test_gpu_parity.py::test_hdiff_ragged_j_chunks_vs_c_oracle runs)."""
+    from test_gpu_parity import RAGGED_CHUNK_OPTS, ragged_chunk_stencil
+
+    for opts in RAGGED_CHUNK_OPTS:
+        src = open(os.path.join(os.path.dirname(_lib_path(ragged_chunk_stencil(opts))), "stencil.hip")).read()
+        assert ("if ((chunk & 1) == 0) {" in src) == bool(opts["jmirror"])
+        assert ("jb + jce - 1 - (" in src) == bool(opts["jmirror"])
+    # no J offsets (copy): nothing to mirror
+    copy = gtscript.stencil(backend="gt:mi355x", definition=sc.copy_stencil, name="gpu.copy_mirror_check",
+                            pointwise_plane=1)
+    src = open(os.path.join(os.path.dirname(_lib_path(copy)), "stencil.hip")).read()
+    assert "chunk & 1" not in src
+
+
 @pytest.mark.parametrize("name", ["hdiff_f64", "tridiag", "higher_dimensional_fields", "staged_forward_ij_temp"])
 def test_library_loads_and_describes_itself(name):
     """The C-ABI library dlopens on a host without a GPU (no compute call is made), reports the

@@ -150,6 +150,36 @@ def test_tridiag_full_size_vs_c_oracle():
         gu.assert_match(storage.to_numpy(devs[k]), ref[k], name=f"tridiag_full:{k}")
 
 
+RAGGED_CHUNK_OPTS = [{"jchunk": 4, "jmirror": 1}, {"jchunk": 8, "jmirror": 1}, {"jchunk": 8, "jmirror": 0}]
+
+
+def ragged_chunk_stencil(opts):
+    from gt4py_amd import gtscript
+
+    return gtscript.stencil(backend=BACKEND, definition=sc.hdiff_f64, name="gpu.hdiff_ragged", **opts)
+
+
+@pytest.mark.parametrize("opts", RAGGED_CHUNK_OPTS, ids=lambda o: f"jc{o['jchunk']}_m{o['jmirror']}")
+@pytest.mark.parametrize("nj", [1, 3, 21, 22, 23, 37])
+def test_hdiff_ragged_j_chunks_vs_c_oracle(opts, nj):
+    """Odd J chunks stream top-down (jmirror): last chunks of every length, both directions."""
+    _torch()
+    from gt4py_amd import storage
+    from oracle import c_oracle
+
+    ni, nk, h = 150, 3, 2
+    stencil = ragged_chunk_stencil(opts)
+    rng = np.random.default_rng(nj)
+    in_h, in_d = _alloc_fill((ni + 2 * h, nj + 2 * h, nk), np.float64, rng, -10, 10, (h, h, 0))
+    co_h, co_d = _alloc_fill((ni, nj, nk), np.float64, rng, 0, 0.5, (0, 0, 0))
+    out_d = storage.zeros((ni, nj, nk), np.float64, backend=BACKEND)
+    org = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    stencil(in_d, out_d, co_d, origin=org, domain=(ni, nj, nk))
+    ref = np.zeros((ni, nj, nk), order="F")
+    c_oracle.horizontal_diffusion(np.asfortranarray(in_h), ref, np.asfortranarray(co_h), org, (ni, nj, nk))
+    gu.assert_match(storage.to_numpy(out_d), ref, name=f"hdiff_ragged_nj{nj}")
+
+
 def test_outside_domain_untouched():
     """Outputs are written inside the compute domain only (stencil_object.py contract)."""
     torch = _torch()
