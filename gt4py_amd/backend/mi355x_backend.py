@@ -79,6 +79,7 @@ class Mi355xBackend(BaseBackend):
         "vector": {"versioning": True, "type": int, "description": "I elements per lane in plane kernels (1, 2, 4)"},
         "prefetch": {"versioning": True, "type": int, "description": "rows loaded ahead in plane kernels"},
         "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
+        "kblock": {"versioning": True, "type": int, "description": "column kernels: window fronts of this many levels loaded together"},
         "col_occupancy": {"versioning": True, "type": int, "description": "max column-kernel blocks per CU (0 = hw)"},
         "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
         "min_blocks": {"versioning": True, "type": int, "description": "plane kernels: __launch_bounds__ min blocks per CU"},
@@ -86,6 +87,8 @@ class Mi355xBackend(BaseBackend):
         "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow)"},
         "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},
         "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},
+        "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
+        "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},

@@ -46,6 +46,13 @@ class ColumnGen:
     def _mem(self, name):
         return name in self.api or name in self.scratch
 
+    def _block(self) -> Tuple[int, int]:
+        """Threads per block in I and J (option ``col_bx``: I width, 256 threads in total)."""
+        bx = int(self.opts.get("col_bx", COLUMN_BLOCK[0]))
+        if bx not in (64, 128, 256):
+            raise ValueError(f"col_bx must be 64, 128 or 256, got {bx}")
+        return bx, (COLUMN_BLOCK[0] * COLUMN_BLOCK[1]) // bx
+
     def _guard(self, li, si, ti) -> Optional[str]:
         """Condition restricting top-level statement ti to its own extent (None: whole region)."""
         (a, b), (c, d) = self.a.extents.blocks.get((li, si, ti), ((0, 0), (0, 0)))
@@ -105,15 +112,24 @@ class ColumnGen:
         L.append("    int32_t ni, nj, nk;")
         L.append("};")
         L.append("")
-        bx, by = COLUMN_BLOCK
+        bx, by = self._block()
         L.append(f"__global__ void __launch_bounds__({bx * by}) k{k}_column(const K{k}Params p) {{")
         if int(self.opts.get("col_occupancy", 0)) > 0:
             L.append("    extern __shared__ __attribute__((aligned(16))) char gtmi_lds_reserve[];")
             L.append("    if (p.ni < 0) gtmi_lds_reserve[threadIdx.x] = 0;  // keep the reservation alive")
         B = []
         eilo, eihi, ejlo, ejhi = self.ext
-        B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x) - {eilo};")
-        B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y) - {ejlo};")
+        if int(self.opts.get("col_order", 0)) == 1:
+            # XCD-aware: consecutive column blocks (along I, then J) run on one XCD (8 XCDs, round-robin dispatch)
+            B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
+            B.append("const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);")
+            B.append("const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;")
+            B.append("const int w = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;")
+            B.append(f"const int i = (w % nbx) * {bx} + (int)threadIdx.x - {eilo};")
+            B.append(f"const int j = (w / nbx) * {by} + (int)threadIdx.y - {ejlo};")
+        else:
+            B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x) - {eilo};")
+            B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y) - {ejlo};")
         B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
         B.append("const int nk = p.nk;")
         for s in scalars:
@@ -134,6 +150,7 @@ class ColumnGen:
         # blocks per CU capped through the LDS reservation: keeps the K-sweep working set of the
         # resident columns small enough to be re-read from the 256 MiB Infinity Cache
         lds = 0 if occ <= 0 else min(160 * 1024, (160 * 1024) // occ - 1024)
+        bx, by = self._block()
         H.append(
             f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
             f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
@@ -204,6 +221,9 @@ class ColumnGen:
             return f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
 
         P = int(self.opts.get("kprefetch", 0))
+        U = int(self.opts.get("kblock", 0))
+        if U > 1:
+            P = 0  # blocked loads replace the rotating prefetch registers
         step = "+" if fwd else "-"
         out = [f"{{  // vertical loop {li} ({order.name})"]
         for (name, di, dj), rng in win.items():
@@ -252,48 +272,6 @@ class ColumnGen:
             out.append(f"    {{  // section {si}")
             out.append(f"        int ks = {lo}, ke = {hi};")
             out.append("        if (ks < 0) ks = 0; if (ke > nk) ke = nk;")
-            if fwd:
-                out.append("        for (int k = ks; k < ke; ++k) {")
-            else:
-                out.append("        for (int k = ke - 1; k >= ks; --k) {")
-            body = []
-            body.append("if (k != k_next) {  // (re)load the full K-window and the prefetch registers")
-            for (name, di, dj), rng in win.items():
-                if not self._mem(name):
-                    continue
-                for d in range(rng[0], rng[1] + 1):
-                    if d == 0 and not zero_needed_in(name, di, dj, sec):
-                        continue
-                    body.append(f"    {wvar(name, di, dj, d)} = {mem_index(name, di, dj, f'k + ({d})')};")
-            for key, fl in front_load.items():
-                if fl:
-                    fd = front[key]
-                    for pp in range(1, P + 1):
-                        body.append(
-                            f"    pf{pp}_{wvar(*key, fd)} = {mem_index(*key, f'k {step} {pp} + ({fd})')};"
-                        )
-            body.append("} else {  // shift the window; its front comes from the prefetch registers")
-            for key, rng in win.items():
-                name, di, dj = key
-                ds = list(range(rng[0], rng[1] + 1))
-                if fwd:
-                    for d in ds[:-1]:
-                        body.append(f"    {wvar(name, di, dj, d)} = {wvar(name, di, dj, d + 1)};")
-                else:
-                    for d in reversed(ds[1:]):
-                        body.append(f"    {wvar(name, di, dj, d)} = {wvar(name, di, dj, d - 1)};")
-                if front_load[key]:
-                    fd = front[key]
-                    fv = wvar(name, di, dj, fd)
-                    if P == 0:
-                        body.append(f"    {fv} = {mem_index(name, di, dj, f'k + ({fd})')};")
-                    else:
-                        body.append(f"    {fv} = pf1_{fv};")
-                        for pp in range(1, P):
-                            body.append(f"    pf{pp}_{fv} = pf{pp + 1}_{fv};")
-                        body.append(f"    pf{P}_{fv} = {mem_index(name, di, dj, f'k {step} {P} + ({fd})')};")
-            body.append("}")
-            body.append(f"k_next = k {step} 1;")
 
             def kaddr(acc: ir.FieldAccess) -> str:
                 kexpr = f"k + ({acc.offset[2]})"
@@ -309,14 +287,90 @@ class ColumnGen:
 
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
             self._kaddr = kaddr
-            for ti, s in enumerate(sec.body):
-                code = self._stmt(s, rend, wvar, mem_store)
-                g = self._guard(li, si, ti)
-                if g:
-                    code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
-                body += code
-            out += ["            " + x for x in body]
-            out.append("        }")
+
+            def level_body(u: Optional[int]) -> List[str]:
+                """One level: window (re)load or shift, then the statements. ``u``: the level's
+                slot in a block of ``U`` levels whose window fronts were loaded together."""
+                body = ["if (k != k_next) {  // (re)load the full K-window and the prefetch registers"]
+                for (name, di, dj), rng in win.items():
+                    if not self._mem(name):
+                        continue
+                    for d in range(rng[0], rng[1] + 1):
+                        if d == 0 and not zero_needed_in(name, di, dj, sec):
+                            continue
+                        body.append(f"    {wvar(name, di, dj, d)} = {mem_index(name, di, dj, f'k + ({d})')};")
+                for key, fl in front_load.items():
+                    if fl:
+                        fd = front[key]
+                        for pp in range(1, P + 1):
+                            body.append(
+                                f"    pf{pp}_{wvar(*key, fd)} = {mem_index(*key, f'k {step} {pp} + ({fd})')};"
+                            )
+                body.append("} else {  // shift the window; its front comes from the prefetch registers")
+                for key, rng in win.items():
+                    name, di, dj = key
+                    ds = list(range(rng[0], rng[1] + 1))
+                    if fwd:
+                        for d in ds[:-1]:
+                            body.append(f"    {wvar(name, di, dj, d)} = {wvar(name, di, dj, d + 1)};")
+                    else:
+                        for d in reversed(ds[1:]):
+                            body.append(f"    {wvar(name, di, dj, d)} = {wvar(name, di, dj, d - 1)};")
+                    if front_load[key]:
+                        fd = front[key]
+                        fv = wvar(name, di, dj, fd)
+                        if u is not None:
+                            body.append(f"    {fv} = bf{u}_{fv};")
+                        elif P == 0:
+                            body.append(f"    {fv} = {mem_index(name, di, dj, f'k + ({fd})')};")
+                        else:
+                            body.append(f"    {fv} = pf1_{fv};")
+                            for pp in range(1, P):
+                                body.append(f"    pf{pp}_{fv} = pf{pp + 1}_{fv};")
+                            body.append(f"    pf{P}_{fv} = {mem_index(name, di, dj, f'k {step} {P} + ({fd})')};")
+                body.append("}")
+                body.append(f"k_next = k {step} 1;")
+                for ti, s in enumerate(sec.body):
+                    code = self._stmt(s, rend, wvar, mem_store)
+                    g = self._guard(li, si, ti)
+                    if g:
+                        code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
+                    body += code
+                return body
+
+            if U > 1:
+                # blocked K loads: the window fronts of U levels are issued together (U independent
+                # loads per stream in flight per wave), then the U levels are computed in order;
+                # levels past the section end re-read its last level (a cache hit, no extra HBM bytes)
+                if fwd:
+                    out.append(f"        for (int kb = ks; kb < ke; kb += {U}) {{")
+                else:
+                    out.append(f"        for (int kb = ke - 1; kb >= ks; kb -= {U}) {{")
+                for key, fl in front_load.items():
+                    if not fl:
+                        continue
+                    fd = front[key]
+                    fv = wvar(*key, fd)
+                    t = decl_dtype[key[0]].ctype
+                    for u in range(U):
+                        kl = f"min(kb + {u}, ke - 1)" if fwd else f"max(kb - {u}, ks)"
+                        out.append(f"            const {t} bf{u}_{fv} = {mem_index(*key, f'{kl} + ({fd})')};")
+                for u in range(U):
+                    cond = f"k < ke" if fwd else "k >= ks"
+                    out.append(f"            {{  // level kb {step} {u}")
+                    out.append(f"                const int k = kb {step} {u};")
+                    out.append(f"                if ({cond}) {{")
+                    out += ["                    " + x for x in level_body(u)]
+                    out.append("                }")
+                    out.append("            }")
+                out.append("        }")
+            else:
+                if fwd:
+                    out.append("        for (int k = ks; k < ke; ++k) {")
+                else:
+                    out.append("        for (int k = ke - 1; k >= ks; --k) {")
+                out += ["            " + x for x in level_body(None)]
+                out.append("        }")
             out.append("    }")
         out.append("}")
         return out
