@@ -82,6 +82,9 @@ def compile_source(source: str, extra_flags: Optional[List[str]] = None, verbose
     so = os.path.join(d, "stencil.so")
     if os.path.exists(so):
         return so
+    if os.environ.get("GTMI_NO_COMPILE"):
+        # set on the GPU box to prove that every library a run needs was prebuilt by build()
+        raise RuntimeError(f"GTMI_NO_COMPILE is set and {so} is not prebuilt")
     os.makedirs(d, exist_ok=True)
     lock_path = os.path.join(d, ".lock")
     with open(lock_path, "w") as lock:
