@@ -192,7 +192,8 @@ class ColumnGen:
                     raise UnsupportedStencil(f"'{name}' written and read at IJ offset in one column loop")
                 rng[0], rng[1] = min(rng[0], 0), max(rng[1], 0)
             if vl.loop_order == ir.LoopOrder.PARALLEL and name in wnames and (rng[0] < 0 or rng[1] > 0):
-                raise UnsupportedStencil(f"'{name}' written and read at a K offset in one PARALLEL loop")
+                if any(_parallel_k_race(sec, name) for sec in vl.sections):
+                    raise UnsupportedStencil(f"'{name}' written and read at a K offset in one PARALLEL loop")
         decl_dtype = {}
         for (name, di, dj) in win:
             decl_dtype[name] = self.st.decl(name).dtype
@@ -416,6 +417,21 @@ class ColumnGen:
             out.append("}")
             return out
         raise TypeError(type(s))
+
+
+def _parallel_k_race(sec: ir.Section, name: str) -> bool:
+    """``name`` written and read at a K offset in a PARALLEL section of more than one static
+    level. A one-level section (``interval(0, 1)``, ``interval(-1, None)``) has no race: it
+    writes its own level only (``gtc/gtir.py:252-262``), so the column sweep may run it."""
+    iv = sec.interval
+    if iv.start.level == iv.end.level and abs(iv.end.offset - iv.start.offset) == 1:
+        return False
+    writes = reads = False
+    for acc, w in iter_accesses(sec.body):
+        if isinstance(acc, ir.FieldAccess) and acc.name == name:
+            writes |= w
+            reads |= (not w) and acc.offset[2] != 0
+    return writes and reads
 
 
 def _sgn(x: int) -> str:

@@ -119,9 +119,11 @@ class _Scope:
 
 
 class StencilParser:
-    def __init__(self, definition, externals: Dict[str, Any], options):
+    def __init__(self, definition, externals: Dict[str, Any], options, dtypes=None):
         self.definition = definition
         self.externals = dict(externals or {})
+        # ``stencil(dtypes=...)``: names usable as types of annotated locals (gtscript_frontend.py:1835-1850)
+        self.dtypes = dict(dtypes or {})
         self.options = options
         self.fields: Dict[str, ir.FieldDecl] = {}
         self.scalars: Dict[str, ir.ScalarDecl] = {}
@@ -288,6 +290,18 @@ class StencilParser:
         def bound(a, is_start):
             if isinstance(a, ast.Constant) and a.value is None:
                 return ir.AxisBound(ir.LevelMarker.START if is_start else ir.LevelMarker.END, 0)
+            runtime = [
+                n.id for n in ast.walk(a)
+                if isinstance(n, ast.Name) and n.id not in scope.imported
+                and (n.id in self.fields or n.id in self.scalars or self._temp_for_local(n.id, scope, create=False))
+            ]
+            if runtime:
+                # RuntimeAxisBound: parsed by the reference frontend, then rejected by the numpy and
+                # gt:* backends (gtc/numpy/oir_to_npir.py:91-94, gtc/gtcpp/oir_to_gtcpp.py:186-196)
+                raise NotImplementedError(
+                    "Runtime interval bounds (e.g. `with interval(0, field)`) is an experimental feature and "
+                    f"not implemented for this backend ({', '.join(runtime)})."
+                )
             v = self._const_eval(a, scope)
             from gt4py_amd.gtscript import AxisIndex
 
@@ -373,7 +387,10 @@ class StencilParser:
         if isinstance(s, ast.AnnAssign):
             if s.value is None:
                 raise GTScriptSyntaxError("Annotated declaration without value")
-            ann = self._const_eval(s.annotation, scope)
+            if isinstance(s.annotation, ast.Name) and s.annotation.id in self.dtypes:
+                ann = self.dtypes[s.annotation.id]
+            else:
+                ann = self._const_eval(s.annotation, scope)
             if isinstance(s.target, ast.Name):
                 from gt4py_amd.gtscript import _FieldDescriptor
 
@@ -1073,8 +1090,8 @@ def _load_copy(target):
     raise GTScriptSyntaxError("Invalid augmented assignment target")
 
 
-def parse_stencil(definition, externals, options) -> ir.Stencil:
-    parser = StencilParser(definition, externals, options)
+def parse_stencil(definition, externals, options, dtypes=None) -> ir.Stencil:
+    parser = StencilParser(definition, externals, options, dtypes)
     stencil = parser.parse()
     stencil.temp_declared_dtype = dict(parser.temp_declared_dtype)
     return stencil

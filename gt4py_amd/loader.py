@@ -34,7 +34,7 @@ class StencilBuilder:
     @functools.cached_property
     def ir(self):
         t0 = time.perf_counter()
-        stencil = frontend.parse_stencil(self.definition, self.externals, self.options)
+        stencil = frontend.parse_stencil(self.definition, self.externals, self.options, self.dtypes)
         if self.options.build_info is not None:
             self.options.build_info["parse_time"] = time.perf_counter() - t0
         return stencil

@@ -546,7 +546,80 @@ def prune_unused_fields(stencil: ir.Stencil) -> ir.Stencil:
     return stencil
 
 
+def _cartesian_h_reads(node) -> Set[str]:
+    """Names read at a non-zero I/J offset (run-time K offsets excluded, ``gtir.py:326-348``)."""
+    return {
+        a.name for a in ir.walk(node)
+        if isinstance(a, ir.FieldAccess) and a.k_offset is None and (a.offset[0] or a.offset[1])
+    }
+
+
+def _assign_writes(stmts) -> Set[str]:
+    out: Set[str] = set()
+    for n in ir.walk(stmts):
+        if isinstance(n, ir.Assign):
+            out |= {a.name for a in ir.walk(n.target) if isinstance(a, ir.FieldAccess)}
+    return out
+
+
+def validate_parallel_model(stencil: ir.Stencil) -> None:
+    """The GTScript parallel-model rules the reference checks while building GTIR.
+
+    Per statement (``gtc/gtir.py:95-109``): no assignment reads its own target at an I/J offset.
+    Per while loop (``:152-166``) and per computation block (``:226-240``; temporaries first
+    assigned in the block exempt): no field is both written and read at an I/J offset. Per
+    PARALLEL block of more than one static level (``:242-300``): a written field is read at its
+    write's K offset only, and never through a run-time K offset or an absolute K index.
+    Blocks are checked in definition order, statements bottom-up, as the validators fire.
+    """
+    temps = {t.name for t in stencil.temporaries}
+    declared: Set[str] = set()
+
+    def check_stmt(s):
+        for child in ir.iter_children(s):
+            if isinstance(child, ir.Stmt):
+                check_stmt(child)
+        if isinstance(s, ir.Assign):
+            if s.target.name in _cartesian_h_reads(s.value):
+                raise ValueError("Self-assignment with offset in I or J is illegal.")
+        elif isinstance(s, ir.While):
+            names = _assign_writes(s.body) & _cartesian_h_reads(s.body)
+            if names:
+                raise ValueError(f"Illegal write and read with horizontal offset detected for {names}.")
+
+    for vl in stencil.vertical_loops:
+        for sec in vl.sections:
+            for s in sec.body:
+                check_stmt(s)
+            written = _assign_writes(sec.body)
+            local = (written & temps) - declared
+            declared |= local
+            bad = (written & _cartesian_h_reads(sec.body)) - local
+            if bad:
+                raise ValueError(f"Illegal write and read with horizontal offset detected for {bad}.")
+            iv = sec.interval
+            size_one = iv.start.level == iv.end.level and abs(iv.end.offset - iv.start.offset) == 1
+            if vl.loop_order != ir.LoopOrder.PARALLEL or size_one:
+                continue
+            writes = [n.target for n in ir.walk(sec.body) if isinstance(n, ir.Assign)]
+            write_ids = {id(w) for w in writes}
+            for node in ir.walk(sec.body):
+                if not isinstance(node, ir.FieldAccess) or id(node) in write_ids:
+                    continue
+                for w in writes:
+                    if node.name != w.name:
+                        continue
+                    if node.k_offset is not None or w.k_offset is not None:
+                        raise ValueError(
+                            "Not allowed to write and read with `VariableKOffset` and/or "
+                            f"`AbsoluteKIndex` in PARALLEL loops: `{node.name}`"
+                        )
+                    if node.offset[2] != w.offset[2]:
+                        raise ValueError(f"Not allowed to write and read with k-offsets in PARALLEL loops: `{node.name}`")
+
+
 def run_pipeline(stencil: ir.Stencil) -> StencilAnalysis:
+    validate_parallel_model(stencil)
     stencil = resolve_dtypes(stencil)
     stencil = upcast(stencil)
     extents = compute_extents(stencil)

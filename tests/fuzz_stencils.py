@@ -115,9 +115,11 @@ def generate(seed):
                 # a PARALLEL temporary is only defined on interval(1, -1): reading it elsewhere reads
                 # uninitialised temporary storage (undefined in GTScript), so stay inside
                 ivl = "interval(1, -1)" if extra else "interval(...)"
+                # one name per computation: a temporary declared in an earlier computation and
+                # written + read at an IJ offset here is illegal (gtc/gtir.py:226-240)
                 L.append(f"    with computation({order}), {ivl}:")
-                L.append(f"        u = {r.choice(NAMES_IN)}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0] * 0.5 + 0.25")
-                L.append(f"        out2 = out2 + 0.5 * (u[1, 0, 0] - u[0, -1, 0]){extra}")
+                L.append(f"        u{ci} = {r.choice(NAMES_IN)}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0] * 0.5 + 0.25")
+                L.append(f"        out2 = out2 + 0.5 * (u{ci}[1, 0, 0] - u{ci}[0, -1, 0]){extra}")
     if not used_out:
         L.append("    with computation(PARALLEL), interval(...):")
         L.append("        out1 = a")
