@@ -4,15 +4,20 @@
 Default workload (``--config hdiff``): ``horizontal_diffusion`` (lap + flux + limiter,
 PARALLEL K) at 2048 x 2048 x 160 fp64 per GPU -- BASELINE.json configs[2], the config the
 metric "Mcells/s + achieved HBM GB/s, horiz-diffusion 2048x2048x160 fp64, 1/2/4/8 GPU" is
-quoted on. With N GPUs (``torch.distributed.run``, one process per GPU) the global domain is
-2048 x (2048*N) x 160 cut into J strips (weak scaling); every step exchanges the 2-row J halo
-of ``in_field`` with the neighbours over RCCL, then runs the stencil on the local strip.
+quoted on. ``--gpus N`` (N > 1) without a torchrun environment starts N ranks itself
+(``torch.distributed.run`` child, one process per GPU) and relays rank 0's line; under torchrun
+each rank owns a 2048 x 2048 x 160 J strip of a 2048 x (2048*N) x 160 global domain (weak
+scaling) and every step exchanges the 2-row J halo of ``in_field`` over RCCL while the interior
+computes.
 
 One step = one stencil application over the whole (local) domain, inputs resident in HBM.
 Timing: W untimed warmups, then K steps bracketed by barrier + synchronize; max over ranks.
 ``roofline`` = algorithmic bytes (24 B/cell: in + coeff read, out written)
-per launch / mean launch time from HIP events on the launch stream. ``cpu_baseline`` = the
-C oracle (cpu_ifirst-equivalent restatement, OpenMP) on a bounded K-slice of the same domain.
+per launch / mean launch time from HIP events on the launch stream; ``traffic`` = rocprofv3
+PMC bytes per launch from ``profiles/pmc_<config>.json`` when that record was measured on the
+same library (build key), else null. ``extra_configs`` (N=1): the other BASELINE configs timed
+in the same process. ``cpu_baseline`` = the C restatement (cpu_ifirst-equivalent, OpenMP) on
+the full domain, median of 20 after 3 warm-ups, in a child process.
 """
 
 
@@ -150,50 +155,323 @@ def stencil_defs():
     }
 
 
-def cpu_baseline(cfg_name, budget_s=10.0):
-    """Time the C oracle (cpu_ifirst-equivalent, OpenMP) on a bounded K-slice sample."""
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline (BASELINE.md "CPU-baseline plan"): the C restatement of the stencil
+# (cpu_ifirst-equivalent, I-first layout, OpenMP over (K, J) rows) on the full domain of the
+# config, median of 20 calls after 3 warm-ups, OMP_PROC_BIND=close / OMP_PLACES=cores. It runs
+# in a child process started after the GPU work so that the OpenMP placement variables are in
+# its environment before libgomp loads.
+# ------------------------------------------------------------------------------------------
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _demo_field(ni, nj, nk, dtype):
+    """The demo analytic field in=5+8*(2+cos(pi(x+1.5y))+sin(2pi(x+1.5y)))/4,
+    constant in K, I-first (Fortran-ordered) host array."""
+    x = np.arange(ni, dtype=np.float64)[:, None] / ni
+    y = np.arange(nj, dtype=np.float64)[None, :] / nj
+    t = x + 1.5 * y
+    plane = (5.0 + 8.0 * (2.0 + np.cos(np.pi * t) + np.sin(2 * np.pi * t)) / 4.0).astype(dtype)
+    arr = np.empty((ni, nj, nk), dtype=dtype, order="F")
+    arr[...] = plane[:, :, None]
+    return arr
+
+
+def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
+    """Body of the ``--cpu-child`` process: time the C oracle on the config's full domain."""
     from oracle import c_oracle
 
     sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[cfg_name]
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    nk_s = max(2, min(nk, 16))
     rng = np.random.default_rng(1337)
+
+    def uni(shape, lo, hi):
+        a = np.empty(shape, dtype=dtype, order="F")
+        for k in range(shape[2]):  # plane by plane: bounded temporaries
+            a[:, :, k] = rng.uniform(lo, hi, shape[:2])
+        return a
+
     if sname == "horizontal_diffusion":
-        a = np.asfortranarray(rng.uniform(-10, 10, (ni + 2 * h, nj + 2 * h, nk_s)).astype(dtype))
-        c = np.asfortranarray(rng.uniform(0, 0.5, (ni, nj, nk_s)).astype(dtype))
-        o = np.zeros((ni, nj, nk_s), dtype=dtype, order="F")
+        a = _demo_field(ni + 2 * h, nj + 2 * h, nk, dtype)
+        c = np.full((ni, nj, nk), 0.025, dtype=dtype, order="F")
+        o = np.zeros((ni, nj, nk), dtype=dtype, order="F")
         org = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
-        fn = lambda: c_oracle.horizontal_diffusion(a, o, c, org, (ni, nj, nk_s), nthreads=threads)  # noqa: E731
+        fn = lambda: c_oracle.horizontal_diffusion(a, o, c, org, (ni, nj, nk), nthreads=threads)  # noqa: E731
+        inputs = "demo analytic in_field, coeff 0.025"
     elif sname == "lap5":
-        a = np.asfortranarray(rng.uniform(-10, 10, (ni + 2, nj + 2, nk_s)))
-        o = np.zeros((ni, nj, nk_s), order="F")
-        fn = lambda: c_oracle.lap5(a, o, {"in_field": (1, 1, 0), "out_field": (0, 0, 0)}, (ni, nj, nk_s), threads)  # noqa: E731
+        a = uni((ni + 2, nj + 2, nk), -10, 10)
+        o = np.zeros((ni, nj, nk), order="F")
+        fn = lambda: c_oracle.lap5(a, o, {"in_field": (1, 1, 0), "out_field": (0, 0, 0)}, (ni, nj, nk), threads)  # noqa: E731
+        inputs = "U(-10,10) seed 1337"
     elif sname == "tridiagonal_solver":
-        arrs = [np.asfortranarray(rng.uniform(lo, hi, (ni, nj, nk_s))) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0))]
+        arrs = [uni((ni, nj, nk), lo, hi) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0))]
         org = {k: (0, 0, 0) for k in ("inf", "diag", "sup", "rhs", "out")}
-        fn = lambda: c_oracle.tridiagonal_solver(*arrs, org, (ni, nj, nk_s), nthreads=threads)  # noqa: E731
+        fn = lambda: c_oracle.tridiagonal_solver(*arrs, org, (ni, nj, nk), nthreads=threads)  # noqa: E731
+        inputs = "diag 4+U[0,1), inf/sup U[-1,1), rhs U[-10,10), seed 1337"
     elif sname == "copy_stencil":
-        a = np.asfortranarray(rng.uniform(-10, 10, (ni, nj, nk_s)))
+        a = uni((ni, nj, nk), -10, 10)
         o = np.zeros_like(a, order="F")
-        fn = lambda: c_oracle.copy_stencil(a, o, {"field_a": (0, 0, 0), "field_b": (0, 0, 0)}, (ni, nj, nk_s), threads)  # noqa: E731
+        fn = lambda: c_oracle.copy_stencil(a, o, {"field_a": (0, 0, 0), "field_b": (0, 0, 0)}, (ni, nj, nk), threads)  # noqa: E731
+        inputs = "U(-10,10) seed 1337"
     else:
-        return None  # no CPU restatement of this stencil in oracle/
-    fn()  # warm-up
-    reps, t0 = 0, time.perf_counter()
-    while True:
+        return {}
+    for _ in range(warm):
         fn()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 5000:
-            break
-    cells = ni * nj * nk_s * reps
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
+    cells = ni * nj * nk
     return {
-        "value": round(cells / el / 1e6, 2),
+        "value": round(cells / med / 1e6, 2),
         "unit": "Mcells/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"C oracle (cpu_ifirst-equivalent, OpenMP) {ni}x{nj}x{nk_s} {np.dtype(dtype).name}, {reps} calls in {el:.1f} s",
+        "ms_per_call": round(med * 1e3, 3),
+        "cpu_model": _cpu_model(),
+        "sample": (f"cpu_ifirst-equivalent (own C++/OpenMP restatement, oracle/cpu_stencils.c) on the full "
+                   f"{ni}x{nj}x{nk} {np.dtype(dtype).name} domain ({inputs}); median of {reps} calls after {warm} "
+                   f"warm-ups; {threads} threads, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
+                   f"OMP_PLACES={os.environ.get('OMP_PLACES')}"),
     }
+
+
+def cpu_baseline(cfg_name: str, reps: int = 20, warm: int = 3, timeout_s: float = 240.0):
+    """Run ``cpu_child`` in a child process (fresh OpenMP runtime with the placement variables)."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", str(os.cpu_count() or 1))
+    env["OMP_PROC_BIND"] = "close"
+    env["OMP_PLACES"] = "cores"
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", cfg_name, "--cpu-reps", str(reps),
+           "--cpu-warm", str(warm)]
+    try:
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"cpu baseline timed out after {timeout_s:.0f} s"}
+    for line in reversed(res.stdout.splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    return {"error": f"cpu baseline child failed (rc {res.returncode}): {res.stderr[-400:]}"}
+
+
+# ------------------------------------------------------------------------------------------
+# Workloads
+# ------------------------------------------------------------------------------------------
+
+
+class Workload:
+    """One config's fields, stencil and step function on this rank."""
+
+    def __init__(self, cfg, args, rank, world, dev, backend, dry_run=False):
+        import torch
+
+        from gt4py_amd import gtscript, storage
+        from gt4py_amd.distributed import Decomposition2D, HaloStencil, HaloStencil2D
+
+        self.cfg = cfg
+        sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[cfg]
+        if dry_run:  # CPU rehearsal of the launcher / rendezvous / halo path: a small tile per rank
+            ni, nj, nk = 64, 32, 8
+        self.sname, self.dtype, self.h, self.bpc = sname, dtype, h, bpc
+        self.global_ij = (ni, nj * world)  # weak scaling: the per-GPU tile is fixed
+        self.dec2d = None
+        if world > 1 and args.decomp == "2d":
+            self.dec2d = Decomposition2D.balanced(self.global_ij[0], self.global_ij[1], world)
+            ni, nj = self.dec2d.local_shape(rank)
+        self.domain = (ni, nj, nk)
+        opts = {} if dry_run else {"device_sync": False}
+        if args.jchunk and not dry_run:
+            opts["jchunk"] = args.jchunk
+        self.stencil = gtscript.stencil(backend=backend, definition=stencil_defs()[(sname, dtype)],
+                                        name=f"bench.{cfg}", externals=EXTERNALS.get(sname, {}), **opts)
+        tdt = storage.torch_dtype(dtype)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1337 + rank)
+
+        def alloc(shape, aligned):
+            if dry_run:  # the numpy backend's own layout, as a torch CPU tensor (the halo path uses torch ops)
+                return torch.from_numpy(storage.empty(shape, dtype, backend=backend, aligned_index=aligned))
+            return storage.empty(shape, dtype, backend=backend, aligned_index=aligned)
+
+        def uniform(shape, lo, hi, aligned=(0, 0, 0)):
+            t = alloc(shape, aligned)
+            t.copy_(torch.rand(shape, generator=gen, device=dev, dtype=tdt) * (hi - lo) + lo)
+            return t
+
+        def zeros(shape):
+            t = alloc(shape, (0, 0, 0))
+            t.zero_()
+            return t
+
+        self.halo = None
+        self.named = None
+        self.params = {}
+        if sname in ("horizontal_diffusion", "lap5"):
+            fin = uniform((ni + 2 * h, nj + 2 * h, nk), -10, 10, (h, h, 0))
+            out = zeros((ni, nj, nk))
+            self.named = {"in_field": fin, "out_field": out}
+            self.origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
+            if sname == "horizontal_diffusion":
+                self.named["coeff"] = uniform((ni, nj, nk), 0.0, 0.5)
+                self.origin["coeff"] = (0, 0, 0)
+            self.args = tuple(self.named.values())
+            overlap = not args.no_overlap
+            if self.dec2d is not None:
+                # 2-D tile: two-phase (corner-correct) exchange on the halo stream, interior overlapped
+                self.halo = HaloStencil2D(self.stencil, ["in_field"], self.dec2d, rank, (h, h), overlap=overlap)
+            elif world > 1:
+                # J strip of the global domain: the in_field halo moves over RCCL while the interior computes
+                self.halo = HaloStencil(self.stencil, ["in_field"], nj, h, rank, world, overlap=overlap)
+            elif args.halo_selfcomm:
+                self.halo = HaloStencil(self.stencil, ["in_field"], nj, h, 0, 1, periodic=True, force_comm=True,
+                                        overlap=overlap)
+        elif sname == "tridiagonal_solver":
+            self.args = tuple(uniform((ni, nj, nk), lo, hi) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0)))
+            self.origin = (0, 0, 0)
+        elif sname == "vertical_advection_dycore":
+            us, ust, upos, ut = (uniform((ni, nj, nk), -1, 1) for _ in range(4))
+            wcon = uniform((ni + 1, nj, nk + 1), -1, 1)
+            self.args = (us, ust, wcon, upos, ut)
+            self.params = {"dtr_stage": 3.0 / 20.0}
+            self.origin = (0, 0, 0)
+        else:
+            self.args = (uniform((ni, nj, nk), -10, 10), zeros((ni, nj, nk)))
+            self.origin = (0, 0, 0)
+        # validate once (full argument checks), then every timed call skips validation
+        self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain)
+
+    def step(self):
+        if self.halo is not None:
+            self.halo(self.named, self.origin, self.domain)
+        else:
+            self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain, validate_args=False)
+
+    def library_key(self):
+        """Content key of the generated library (``.gt_cache/gt_mi355x/<key>/stencil.so``)."""
+        compiled = getattr(getattr(self.stencil, "_gt_run_impl_", None), "compiled", None)
+        if compiled is None:
+            return None
+        return os.path.basename(os.path.dirname(compiled.lib_path))
+
+
+def time_workload(wl, steps, warmup, dev, dist=None, events=True):
+    """W untimed warm-ups, then K steps bracketed by barrier + synchronize; returns (elapsed s,
+    mean per-launch kernel ms from HIP events on the launch stream, or None)."""
+    import torch
+
+    cuda = dev.type == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    for _ in range(warmup):
+        wl.step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    evs = None
+    if cuda and events:
+        # events on torch's current stream: gtmi_stencil_run enqueues on that stream
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s in range(steps):
+        if evs is not None:
+            evs[s][0].record()
+        wl.step()
+        if evs is not None:
+            evs[s][1].record()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs is not None else None
+    return elapsed, kernel_ms
+
+
+def traffic_for(cfg, key):
+    """HBM bytes per launch from ``profiles/pmc_<cfg>.json`` -- only when that measurement was
+    taken on the library this run executed (same build key); otherwise null plus the reason."""
+    path = os.path.join(REPO, "profiles", f"pmc_{cfg}.json")
+    if not os.path.exists(path):
+        return None, "no pmc measurement for this config"
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None, "unreadable pmc record"
+    if key is None or rec.get("build_key") != key:
+        return None, f"pmc record is for library {rec.get('build_key')}, this run executed {key}"
+    return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_{cfg}.json (library {key})"
+
+
+EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv")
+
+
+# ------------------------------------------------------------------------------------------
+# Launcher: `bench.py --gpus N` without a torchrun environment starts the N ranks itself
+# ------------------------------------------------------------------------------------------
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv) -> int:
+    """Start ``args.gpus`` ranks with torch.distributed.run (one process per GPU) as a CHILD
+    process -- this process never touches the GPU, so nothing here initialises HIP before the
+    ranks exist -- and relay rank 0's single JSON line. Non-zero exit if any rank fails."""
+    import subprocess
+
+    n = args.gpus
+    if not args.dry_run:
+        import torch  # device_count() does not initialise HIP on this image
+
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            print(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible", file=sys.stderr)
+            return 2
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.dry_run:
+        env["GTMI_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    res = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith('{"metric"')]
+    if res.returncode != 0 or len(lines) != 1:
+        sys.stderr.write(res.stdout)
+        print(f"bench.py: {n}-rank run failed (rc {res.returncode}, {len(lines)} result lines)", file=sys.stderr)
+        return res.returncode or 1
+    rec = json.loads(lines[0])
+    if rec.get("n_gpus") != n:
+        print(f"bench.py: ranks reported n_gpus={rec.get('n_gpus')}, expected {n}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+# ------------------------------------------------------------------------------------------
 
 
 def main():
@@ -203,7 +481,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="hdiff", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-extra", action="store_true", help="N=1: skip the extra_configs timings")
+    ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--jchunk", type=int, default=None)
     ap.add_argument("--decomp", default="jstrips", choices=["jstrips", "2d"],
                     help="N>1: J strips (default) or a balanced 2-D process grid (corners exchanged)")
@@ -212,7 +491,26 @@ def main():
     ap.add_argument("--halo-selfcomm", action="store_true",
                     help="N=1 under torchrun: run the J-strip halo path with the rank as its own periodic "
                          "neighbour through RCCL (measures the per-rank cost of the exchange + split)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal: numpy backend, gloo, a 64x32x8 tile per rank (no GPU)")
+    ap.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-reps", type=int, default=20, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-warm", type=int, default=3, help=argparse.SUPPRESS)
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+
+    if args.cpu_child:
+        print(json.dumps(cpu_child(args.cpu_child, args.cpu_reps, args.cpu_warm)), flush=True)
+        return 0
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch(args, argv)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
 
     # exactly one JSON line on stdout: native libraries (RCCL's version banner, ...) write to fd 1,
     # so fd 1 is pointed at stderr for the whole run and the result goes to a saved copy of it
@@ -222,138 +520,46 @@ def main():
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a ROCm GPU")
-    ndev = torch.cuda.device_count()
-    torch.cuda.set_device(local_rank % ndev)
-    dev = torch.device("cuda", local_rank % ndev)
+    if args.dry_run:
+        dev = torch.device("cpu")
+        backend = "numpy"
+    else:
+        if not torch.cuda.is_available():
+            raise SystemExit("bench.py needs a ROCm GPU (use --dry-run for the CPU rehearsal)")
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local_rank % ndev)
+        dev = torch.device("cuda", local_rank % ndev)
+        backend = "gt:mi355x"
     dist = None
     if world > 1 or args.halo_selfcomm:
         from gt4py_amd.distributed import init_process_group
 
-        # nccl (= RCCL over xGMI) on a real node; GTMI_DIST_BACKEND=gloo rehearses N ranks on one GPU.
+        # nccl (= RCCL over xGMI) on a real node; GTMI_DIST_BACKEND=gloo rehearses N ranks.
         # Keep RCCL's version banner off stdout: rank 0 prints exactly one JSON line there.
         os.environ.setdefault("NCCL_DEBUG", "WARN")
-        init_process_group(os.environ.get("GTMI_DIST_BACKEND", "nccl"))
+        init_process_group("gloo" if args.dry_run else os.environ.get("GTMI_DIST_BACKEND", "nccl"))
         import torch.distributed as dist
 
-    from gt4py_amd import gtscript, storage
-    from gt4py_amd.distributed import Decomposition2D, HaloStencil, HaloStencil2D
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
 
-    sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[args.config]
-    # weak scaling: the per-GPU tile is fixed, the global domain is ni x (nj * world)
-    global_ij = (ni, nj * world)
-    dec2d = None
-    if world > 1 and args.decomp == "2d":
-        dec2d = Decomposition2D.balanced(global_ij[0], global_ij[1], world)
-        ni, nj = dec2d.local_shape(rank)
-    defs = stencil_defs()
-    opts = {"device_sync": False}
-    if args.jchunk:
-        opts["jchunk"] = args.jchunk
-    externals = EXTERNALS.get(sname, {})
-    stencil = gtscript.stencil(backend="gt:mi355x", definition=defs[(sname, dtype)], name=f"bench.{args.config}",
-                               externals=externals, **opts)
-
-    be = "gt:mi355x"
-    tdt = storage.torch_dtype(dtype)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1337 + rank)
-
-    def uniform(shape, lo, hi, aligned):
-        t = storage.empty(shape, dtype, backend=be, aligned_index=aligned)
-        t.copy_(torch.rand(shape, generator=gen, device=dev, dtype=tdt) * (hi - lo) + lo)
-        return t
-
-    halo = None
-    call_params = {}
-    if sname == "horizontal_diffusion" or sname == "lap5":
-        fin = uniform((ni + 2 * h, nj + 2 * h, nk), -10, 10, (h, h, 0))
-        out = storage.zeros((ni, nj, nk), dtype, backend=be)
-        if sname == "horizontal_diffusion":
-            coeff = uniform((ni, nj, nk), 0.0, 0.5, (0, 0, 0))
-            call_args = (fin, out, coeff)
-            named = {"in_field": fin, "out_field": out, "coeff": coeff}
-            origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
-        else:
-            call_args = (fin, out)
-            named = {"in_field": fin, "out_field": out}
-            origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
-        if dec2d is not None:
-            # 2-D tile: two-phase (corner-correct) exchange on the halo stream, interior overlapped
-            halo = HaloStencil2D(stencil, ["in_field"], dec2d, rank, (h, h), overlap=not args.no_overlap)
-        elif world > 1:
-            # J-strip of the global domain: exchange the in_field halo with the neighbours over
-            # RCCL while the interior rows compute, then the two boundary strips
-            halo = HaloStencil(stencil, ["in_field"], nj, h, rank, world, overlap=not args.no_overlap)
-        elif args.halo_selfcomm:
-            halo = HaloStencil(stencil, ["in_field"], nj, h, 0, 1, periodic=True, force_comm=True,
-                               overlap=not args.no_overlap)
-    elif sname == "tridiagonal_solver":
-        fields = [uniform((ni, nj, nk), lo, hi, (0, 0, 0)) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0))]
-        call_args = tuple(fields)
-        origin = (0, 0, 0)
-    elif sname == "vertical_advection_dycore":
-        us, ust, upos, ut = (uniform((ni, nj, nk), -1, 1, (0, 0, 0)) for _ in range(4))
-        wcon = uniform((ni + 1, nj, nk + 1), -1, 1, (0, 0, 0))
-        call_args = (us, ust, wcon, upos, ut)
-        call_params = {"dtr_stage": 3.0 / 20.0}
-        origin = (0, 0, 0)
-    else:
-        a = uniform((ni, nj, nk), -10, 10, (0, 0, 0))
-        b = storage.zeros((ni, nj, nk), dtype, backend=be)
-        call_args = (a, b)
-        origin = (0, 0, 0)
-    domain = (ni, nj, nk)
-
-    def step(ev_pair=None):
-        if ev_pair is not None:
-            ev_pair[0].record()
-        if halo is not None:
-            halo(named, origin, domain)
-        else:
-            stencil(*call_args, **call_params, origin=origin, domain=domain, validate_args=False)
-        if ev_pair is not None:
-            ev_pair[1].record()
-
-    # validate once (full checks), then warm up
-    stencil(*call_args, **call_params, origin=origin, domain=domain)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(evs[s])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    wl = Workload(args.config, args, rank, world, dev, backend, dry_run=args.dry_run)
+    elapsed, kernel_ms = time_workload(wl, args.steps, args.warmup, dev, dist)
     if dist is not None:
         tdev = dev if str(dist.get_backend()).lower() == "nccl" else "cpu"
-        t = torch.tensor([elapsed, kernel_ms], device=tdev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kernel_ms or 0.0], device=tdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed, kernel_ms = float(t[0]), (float(t[1]) if kernel_ms is not None else None)
+    ni, nj, nk = wl.domain
     cells_per_step = ni * nj * nk
-    total_cells = global_ij[0] * global_ij[1] * nk * args.steps
+    total_cells = wl.global_ij[0] * wl.global_ij[1] * nk * args.steps
     value = total_cells / elapsed / 1e6
-    achieved_gbs = cells_per_step * bpc / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    key = None if args.dry_run else wl.library_key()
+    traffic, traffic_src = (None, "dry run") if args.dry_run else traffic_for(args.config, key)
+    kms = kernel_ms if kernel_ms else elapsed / args.steps * 1e3
+    achieved_gbs = cells_per_step * wl.bpc / (kms * 1e-3) / 1e9
+    dec2d = wl.dec2d
     result = {
         "metric": "Mcells/s + achieved HBM GB/s, horiz-diffusion 2048x2048x160 fp64, 1/2/4/8 GPU",
         "value": round(value, 2),
@@ -365,20 +571,20 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {np.float64: "f64", np.float32: "f32"}[dtype],
+        "dtype": {np.float64: "f64", np.float32: "f32"}[wl.dtype],
         "data": "synthetic (uniform random fields generated on device)",
         "config": {
-            "workload": f"{sname} {ni}x{nj}x{nk} {np.dtype(dtype).name} per GPU"
+            "workload": f"{wl.sname} {ni}x{nj}x{nk} {np.dtype(wl.dtype).name} per GPU"
             + (
                 f", {'J-strips' if dec2d is None else f'{dec2d.pi}x{dec2d.pj} tiles'} of a "
-                f"{global_ij[0]}x{global_ij[1]}x{nk} global domain, RCCL halo {h}"
+                f"{wl.global_ij[0]}x{wl.global_ij[1]}x{nk} global domain, RCCL halo {wl.h}"
                 if world > 1
                 else ""
             ),
-            "stencil": sname,
+            "stencil": wl.sname,
             "domain_per_gpu": [ni, nj, nk],
-            "global_domain": [global_ij[0], global_ij[1], nk],
-            "backend": "gt:mi355x",
+            "global_domain": [wl.global_ij[0], wl.global_ij[1], nk],
+            "backend": backend,
             "parallelism": (f"ij-strips{world}" if dec2d is None else f"ij-tiles{dec2d.pi}x{dec2d.pj}")
             if world > 1
             else ("single+halo-selfcomm" if args.halo_selfcomm else "single"),
@@ -390,20 +596,57 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel_ms": round(kernel_ms, 4),
-            "algorithmic_bytes_per_cell": bpc,
+            "traffic_source": traffic_src,
+            "kernel_ms": round(kernel_ms, 4) if kernel_ms is not None else None,
+            "algorithmic_bytes_per_cell": wl.bpc,
+            "library": key,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args.config, args.cpu_budget)
-        if cb is not None:
+    if args.dry_run:
+        result["dry_run"] = True
+        result["data"] = "synthetic; DRY RUN on CPU (numpy backend, gloo): not a measurement"
+    del wl
+    if world == 1 and not args.dry_run and not args.no_extra and not args.halo_selfcomm:
+        # the other BASELINE configs, timed in the same process after the headline (C2, C4, the C5
+        # per-GPU tile, copy, vadv): per-launch kernel time from HIP events, fraction of 8 TB/s
+        extra = {}
+        for cfg in EXTRA_CONFIGS:
+            if cfg == args.config:
+                continue
+            try:
+                w = Workload(cfg, args, 0, 1, dev, backend)
+                el, kms_x = time_workload(w, args.extra_steps, 3, dev)
+                n_i, n_j, n_k = w.domain
+                gbs = n_i * n_j * n_k * w.bpc / (kms_x * 1e-3) / 1e9
+                tr, _ = traffic_for(cfg, w.library_key())
+                extra[cfg] = {
+                    "workload": f"{w.sname} {n_i}x{n_j}x{n_k} {np.dtype(w.dtype).name}",
+                    "ms": round(el / args.extra_steps * 1e3, 4),
+                    "kernel_ms": round(kms_x, 4),
+                    "Mcells_s": round(n_i * n_j * n_k / (kms_x * 1e-3) / 1e6, 1),
+                    "achieved_GBs": round(gbs, 1),
+                    "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "algorithmic_bytes_per_cell": w.bpc,
+                    "traffic": tr,
+                    "library": w.library_key(),
+                }
+                del w
+            except Exception as e:  # noqa: BLE001 - one failing extra config must not hide the headline
+                extra[cfg] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        result["extra_configs"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        cb = cpu_baseline(args.config)
+        if cb:
             result["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

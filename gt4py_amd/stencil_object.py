@@ -484,6 +484,7 @@ def make_stencil_class(
         "_gt_constants_": constants,
         "_gt_options_": options,
         "_gt_id_": stencil_id,
+        "_gt_run_impl_": staticmethod(run_impl),  # backend hook (gt:mi355x: .compiled.lib_path)
         "definition_func": staticmethod(definition_func),
         "__module__": module,
         "__doc__": inspect.getdoc(definition_func) or "",

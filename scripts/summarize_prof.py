@@ -59,6 +59,8 @@ def main(prof_dir, tag):
                 json.dump({
                     "config": cfg,
                     "workload": e["workload"],
+                    # bench.py reports this record's bytes only for the library it was measured on
+                    "build_key": e["roofline"].get("library"),
                     "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
                     "fetch_size_kib": round(fetch, 1),
                     "write_size_kib": round(write, 1),

@@ -1,0 +1,45 @@
+"""bench.py contract on CPU: ``--gpus N`` starts N ranks itself (no torchrun environment) and
+relays exactly one JSON line with ``n_gpus == N``; a WORLD_SIZE / --gpus mismatch is an error.
+The ``--dry-run`` mode runs the same launcher, rendezvous (gloo, 127.0.0.1) and halo-exchange
+path on the numpy backend, so this needs no GPU."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout, cwd=REPO)
+
+
+@pytest.mark.parametrize("gpus,decomp", [(1, "jstrips"), (2, "jstrips"), (2, "2d"), (3, "jstrips")])
+def test_bench_launcher_dry_run(gpus, decomp):
+    res = _run(["--dry-run", "--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--decomp", decomp])
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, res.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == gpus
+    assert rec["dry_run"] is True
+    assert rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["global_domain"][1] == 32 * gpus
+    if gpus > 1:
+        assert rec["config"]["parallelism"].startswith("ij-")
+    for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "roofline", "config"):
+        assert key in rec
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    res = _run(["--dry-run", "--gpus", "2"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert res.returncode == 2
+    assert "WORLD_SIZE" in res.stderr
