@@ -78,15 +78,14 @@ class Mi355xBackend(BaseBackend):
         "jchunk": {"versioning": True, "type": int, "description": "J rows per wavefront in plane kernels (0 = auto)"},
         "vector": {"versioning": True, "type": int, "description": "I elements per lane in plane kernels (1, 2, 4)"},
         "prefetch": {"versioning": True, "type": int, "description": "rows loaded ahead in plane kernels"},
-        "kprefetch": {"versioning": True, "type": int, "description": "levels loaded ahead in column kernels"},
-        "kblock": {"versioning": True, "type": int, "description": "column kernels: window fronts of this many levels loaded together"},
-        "col_occupancy": {"versioning": True, "type": int, "description": "max column-kernel blocks per CU (0 = hw)"},
         "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
         "min_blocks": {"versioning": True, "type": int, "description": "plane kernels: __launch_bounds__ min blocks per CU"},
         "pointwise_plane": {"versioning": True, "type": int, "description": "stream pointwise PARALLEL loops with K1"},
         "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow)"},
         "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},
         "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},
+        "kring": {"versioning": True, "type": int, "description": "column kernels: window-front loads in flight (levels)"},
+        "ktail_lds": {"versioning": True, "type": int, "description": "column kernels: LDS bytes for the sweep-to-sweep tail cache (0 = off)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},

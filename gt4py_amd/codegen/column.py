@@ -1,25 +1,63 @@
 """K2 -- the column kernel generator (FORWARD/BACKWARD sweeps, K-windows in registers).
 
-See ``codegen/hip.py`` for the skeleton's description and DESIGN.md §3.
+One thread per (i, j) column, 64 x 4 threads per block; the thread walks the levels of each
+vertical loop of the kernel in loop order. See ``codegen/hip.py`` and DESIGN.md §3.
+
+* **K-windows** -- every accessed ``(name, di, dj)`` has a register window over the K offsets
+  it is read at (the register-carried K-cache of the reference's ``KCacheDetection``,
+  ``gtc/passes/oir_optimizations/caches.py:92``): a level loads only the window *front*.
+* **Load ring** -- the fronts of the next ``kring`` levels are in flight at any time: each
+  section runs in blocks of ``kring`` levels unrolled over statically indexed ring slots
+  (slot ``u`` holds the front of level ``kb + u``); after level ``k`` computes, its slot is
+  refilled with level ``k + kring``. Fronts never alias a pending write: a loop writes a
+  field only at its own level, and fronts lie ahead of the sweep.
+* **Sweep-to-sweep tail cache** -- when a FORWARD (or PARALLEL) loop is followed in the same
+  kernel by a BACKWARD loop (or the reverse) that reads, at ``(0, 0)``, fields the first loop
+  holds in its windows (the Thomas solve's ``c'``/``d'``: ``sup``/``rhs``; vadv's ``ccol``,
+  ``dcol``, ``u_pos``), the values of the LAST ``L`` levels of the first sweep -- the FIRST
+  levels of the second -- are kept in LDS, so the second sweep re-reads only the remaining
+  ``nk - L`` levels from HBM. The reference's ``gt:gpu`` re-reads every level there (its
+  backward multistage k-caches only the field it writes). ``L`` = LDS budget / (256 threads x
+  cached bytes per level), capped at ``nk``; scratch temporaries only these two loops use are
+  not written to memory at the cached levels at all.
 """
 
 from __future__ import annotations
 
 import dataclasses
-import math
 from typing import Dict, List, Optional, Set, Tuple
 
 from gt4py_amd import ir
-from gt4py_amd.codegen.plan import ColumnKernel, KernelPlan, PlaneKernel, UnsupportedStencil
-from gt4py_amd.ir import DataType
-from gt4py_amd.passes import ZERO_EXTENT, StencilAnalysis, iter_accesses
+from gt4py_amd.codegen.plan import ColumnKernel, KernelPlan, UnsupportedStencil
+from gt4py_amd.passes import StencilAnalysis, iter_accesses
 from gt4py_amd.codegen.common import (  # noqa: F401
-    COLUMN_BLOCK, PLANE_BLOCK_WAVES, WAVE, ExprRenderer, FieldSlot, cname, host_fill, interval_bounds, kparam_decl,
-    literal, region_condition,
+    COLUMN_BLOCK, ExprRenderer, FieldSlot, cname, host_fill, interval_bounds, kparam_decl, region_condition,
 )
 
-# K2: column kernel
-# ------------------------------------------------------------------------------------------
+LDS_BYTES = 160 * 1024  # per CU (MI355X_MICROARCH.md); one 256-thread block may take all of it
+DEFAULT_RING = 8
+
+
+@dataclasses.dataclass
+class _LoopInfo:
+    fwd: bool
+    direct: Set[str]
+    win: Dict[Tuple[str, int, int], List[int]]  # (name, di, dj) -> [dmin, dmax]
+    wnames: Set[str]  # window names written in the loop
+
+
+@dataclasses.dataclass
+class _Tail:
+    """LDS tail cache between loops ``a`` and ``b`` (consecutive in the kernel, opposite sweeps)."""
+
+    a: int
+    b: int
+    a_fwd: bool
+    fields: List[str]
+    no_store: Set[str]  # scratch fields whose cached levels are never written to memory
+
+    def var(self, name):
+        return f"tl_{cname(name)}"
 
 
 class ColumnGen:
@@ -42,6 +80,9 @@ class ColumnGen:
                     (a, b), (c, d) = analysis.extents.blocks.get((li, si, ti), ((0, 0), (0, 0)))
                     ilo, ihi, jlo, jhi = max(ilo, a), max(ihi, b), max(jlo, c), max(jhi, d)
         self.ext = (ilo, ihi, jlo, jhi)
+        self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
+        self.info = {li: self._analyse_loop(li) for li in kernel.loops}
+        self.tail = self._plan_tail()
 
     def _mem(self, name):
         return name in self.api or name in self.scratch
@@ -68,6 +109,94 @@ class ColumnGen:
             conds.append(f"j < p.nj + {d}")
         return " && ".join(conds) if conds else None
 
+    # ------------------------------------------------------------------ analysis
+    def _analyse_loop(self, li) -> _LoopInfo:
+        vl = self.st.vertical_loops[li]
+        # direct fields: read at a run-time K offset or written at a K offset in this loop; every
+        # access to them goes to memory at its own address (no register window)
+        direct: Set[str] = set()
+        for sec in vl.sections:
+            for acc, w in iter_accesses(sec.body):
+                if isinstance(acc, ir.FieldAccess) and (acc.k_offset is not None or (w and acc.offset[2] != 0)):
+                    if not self._mem(acc.name):
+                        raise UnsupportedStencil(f"run-time or written K offset on temporary '{acc.name}'")
+                    direct.add(acc.name)
+        win: Dict[Tuple[str, int, int], List[int]] = {}
+        wnames: Set[str] = set()
+        for sec in vl.sections:
+            for acc, w in iter_accesses(sec.body):
+                if not isinstance(acc, ir.FieldAccess) or acc.name in direct:
+                    continue
+                di, dj, dk = acc.offset
+                rng = win.setdefault((acc.name, di, dj), [dk, dk])
+                rng[0], rng[1] = min(rng[0], dk), max(rng[1], dk)
+                if w:
+                    wnames.add(acc.name)
+        for (name, di, dj), rng in win.items():
+            if name in wnames:
+                if di or dj:
+                    raise UnsupportedStencil(f"'{name}' written and read at IJ offset in one column loop")
+                rng[0], rng[1] = min(rng[0], 0), max(rng[1], 0)
+            if vl.loop_order == ir.LoopOrder.PARALLEL and name in wnames and (rng[0] < 0 or rng[1] > 0):
+                if any(_parallel_k_race(sec, name) for sec in vl.sections):
+                    raise UnsupportedStencil(f"'{name}' written and read at a K offset in one PARALLEL loop")
+            if not self._mem(name) and rng[0] != rng[1] and not _contiguous(vl):
+                # a register-only value read at another level across a gap between sections: the
+                # gap levels never run, so the window cannot carry it (staged lowering puts it in scratch)
+                raise UnsupportedStencil(f"register temporary '{name}' read at a K offset across a section gap")
+        return _LoopInfo(vl.loop_order != ir.LoopOrder.BACKWARD, direct, win, wnames)
+
+    def _plan_tail(self) -> Optional[_Tail]:
+        budget = int(self.opts.get("ktail_lds", LDS_BYTES))
+        if budget <= 0 or any(self.ext):
+            return None
+        loops = self.kernel.loops
+        best = None
+        for x in range(len(loops) - 1):
+            la, lb = loops[x], loops[x + 1]
+            A, B = self.info[la], self.info[lb]
+            vla = self.st.vertical_loops[la]
+            if A.fwd == B.fwd or not _covers_all_levels(vla, A.fwd):
+                continue
+            b_written = {acc.name for sec in self.st.vertical_loops[lb].sections
+                         for acc, w in iter_accesses(sec.body) if w}
+            fields = []
+            for (name, di, dj) in B.win:
+                if (di, dj) != (0, 0) or not self._mem(name) or name in b_written or name in B.direct:
+                    continue
+                if "K" not in self.st.decl(name).axes:  # one value for all levels: nothing per level to cache
+                    continue
+                if any(k[0] == name and (k[1], k[2]) != (0, 0) for k in B.win):
+                    continue
+                rng = A.win.get((name, 0, 0))
+                if rng is None or name in A.direct or not (rng[0] <= 0 <= rng[1]):
+                    continue
+                fields.append(name)
+            if fields and (best is None or len(fields) > len(best.fields)):
+                # scratch values only these two loops touch need no memory copy of the cached levels
+                no_store = set()
+                for n in fields:
+                    if n in self.scratch and self._touching_loops(n) <= {la, lb}:
+                        no_store.add(n)
+                best = _Tail(la, lb, A.fwd, fields, no_store)
+        if best is None:
+            return None
+        per_level = 256 * sum(self.st.decl(n).dtype.itemsize for n in best.fields)
+        self.tail_lmax = budget // per_level
+        if self.tail_lmax < 1:
+            return None
+        self.tail_per_level = per_level
+        return best
+
+    def _touching_loops(self, name) -> Set[int]:
+        out = set()
+        for li, vl in enumerate(self.st.vertical_loops):
+            for sec in vl.sections:
+                if any(acc.name == name for acc, _ in iter_accesses(sec.body)):
+                    out.add(li)
+        return out
+
+    # ------------------------------------------------------------------ rendering
     def render(self) -> Tuple[str, str]:
         k = self.kid
         st = self.st
@@ -110,13 +239,11 @@ class ColumnGen:
         for s in scalars:
             L.append(f"    {s.dtype.ctype} s_{cname(s.name)};")
         L.append("    int32_t ni, nj, nk;")
+        L.append("    int32_t tail_len;  // levels held in the LDS tail cache (0: none)")
         L.append("};")
         L.append("")
         bx, by = self._block()
         L.append(f"__global__ void __launch_bounds__({bx * by}) k{k}_column(const K{k}Params p) {{")
-        if int(self.opts.get("col_occupancy", 0)) > 0:
-            L.append("    extern __shared__ __attribute__((aligned(16))) char gtmi_lds_reserve[];")
-            L.append("    if (p.ni < 0) gtmi_lds_reserve[threadIdx.x] = 0;  // keep the reservation alive")
         B = []
         eilo, eihi, ejlo, ejhi = self.ext
         if int(self.opts.get("col_order", 0)) == 1:
@@ -134,6 +261,33 @@ class ColumnGen:
         B.append("const int nk = p.nk;")
         for s in scalars:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
+        # column base pointers: the i/j part of every address, computed once per thread
+        self.bases: Dict[Tuple[str, int, int], str] = {}
+        for li in self.kernel.loops:
+            inf = self.info[li]
+            for (name, di, dj) in list(inf.win) + [(n, None, None) for n in sorted(inf.direct)]:
+                if not self._mem(name):
+                    continue
+                if di is None:
+                    continue  # direct accesses: offsets known per access, see _base()
+                self._base(name, di, dj, B, name in written)
+            for sec in self.st.vertical_loops[li].sections:
+                for acc, w in iter_accesses(sec.body):
+                    if isinstance(acc, ir.FieldAccess) and acc.name in inf.direct:
+                        self._base(acc.name, acc.offset[0], acc.offset[1], B, acc.name in written)
+        if self.tail is not None:
+            t = self.tail
+            B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
+            B.append(f"const int tid = (int)(threadIdx.y * {bx} + threadIdx.x);")
+            if t.a_fwd:
+                B.append("const int tc0 = nk - p.tail_len, tc1 = nk;  // cached levels [tc0, tc1)")
+            else:
+                B.append("const int tc0 = 0, tc1 = p.tail_len;  // cached levels [tc0, tc1)")
+            off = "0"
+            for n in t.fields:
+                ct = self.st.decl(n).dtype.ctype
+                B.append(f"{ct}* __restrict__ {t.var(n)} = ({ct}*)(gtmi_lds + {off});")
+                off = f"{off} + (size_t)p.tail_len * 256 * sizeof({ct})"
         for li in self.kernel.loops:
             B += self._render_loop(li)
         L += ["    " + x for x in B]
@@ -146,11 +300,18 @@ class ColumnGen:
         for i_s, s in enumerate(scalars):
             H.append(f"        memcpy(&p.s_{cname(s.name)}, &sc[{i_s}], sizeof(p.s_{cname(s.name)}));")
         H.append("        p.ni = ni; p.nj = nj; p.nk = nk;")
-        occ = int(self.opts.get("col_occupancy", 0))
-        # blocks per CU capped through the LDS reservation: keeps the K-sweep working set of the
-        # resident columns small enough to be re-read from the 256 MiB Infinity Cache
-        lds = 0 if occ <= 0 else min(160 * 1024, (160 * 1024) // occ - 1024)
-        bx, by = self._block()
+        lds = "0"
+        if self.tail is not None:
+            H.append(f"        p.tail_len = nk < {self.tail_lmax} ? nk : {self.tail_lmax};")
+            lds = f"(size_t)p.tail_len * {self.tail_per_level}"
+            H.append("        static bool lds_attr = false;")
+            H.append("        if (!lds_attr) {")
+            H.append(f"            hipFuncSetAttribute((const void*)k{k}_column, hipFuncAttributeMaxDynamicSharedMemorySize, "
+                     f"{LDS_BYTES});")
+            H.append("            lds_attr = true;")
+            H.append("        }")
+        else:
+            H.append("        p.tail_len = 0;")
         H.append(
             f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
             f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
@@ -159,41 +320,31 @@ class ColumnGen:
         H.append("}")
         return "\n".join(L), "\n".join(H)
 
+    def _base(self, name, di, dj, out: List[str], writable: bool) -> str:
+        key = (name, di, dj)
+        if key not in self.bases:
+            c = cname(name)
+            v = f"cb_{c}_{_sgn(di)}_{_sgn(dj)}"
+            t = self.st.decl(name).dtype.ctype
+            const = "" if writable else "const "
+            out.append(
+                f"{const}{t}* __restrict__ {v} = p.p_{c} + ((int64_t)gtmi::clampi(i + ({di}), p.ilo_{c}, p.ihi_{c}) * "
+                f"p.sI_{c} + (int64_t)gtmi::clampi(j + ({dj}), p.jlo_{c}, p.jhi_{c}) * p.sJ_{c});"
+            )
+            self.bases[key] = v
+        return self.bases[key]
+
     def _render_loop(self, li) -> List[str]:
         vl = self.st.vertical_loops[li]
         order = vl.loop_order
-        fwd = order != ir.LoopOrder.BACKWARD
-        # direct fields: read at a run-time K offset or written at a K offset in this loop; every
-        # access to them goes to memory at its own address (no register window)
-        direct: Set[str] = set()
-        for sec in vl.sections:
-            for acc, w in iter_accesses(sec.body):
-                if isinstance(acc, ir.FieldAccess) and (acc.k_offset is not None or (w and acc.offset[2] != 0)):
-                    if not self._mem(acc.name):
-                        raise UnsupportedStencil(f"run-time or written K offset on temporary '{acc.name}'")
-                    direct.add(acc.name)
+        info = self.info[li]
+        fwd = info.fwd
+        direct, win, wnames = info.direct, info.win, info.wnames
         self.direct = direct
-        # windows: key (name, di, dj) -> [dmin, dmax]
-        win: Dict[Tuple[str, int, int], List[int]] = {}
-        wnames: Set[str] = set()
-        for sec in vl.sections:
-            for acc, w in iter_accesses(sec.body):
-                if not isinstance(acc, ir.FieldAccess) or acc.name in direct:
-                    continue
-                di, dj, dk = acc.offset
-                key = (acc.name, di, dj)
-                rng = win.setdefault(key, [dk, dk])
-                rng[0], rng[1] = min(rng[0], dk), max(rng[1], dk)
-                if w:
-                    wnames.add(acc.name)
-        for (name, di, dj), rng in win.items():
-            if name in wnames:
-                if di or dj:
-                    raise UnsupportedStencil(f"'{name}' written and read at IJ offset in one column loop")
-                rng[0], rng[1] = min(rng[0], 0), max(rng[1], 0)
-            if vl.loop_order == ir.LoopOrder.PARALLEL and name in wnames and (rng[0] < 0 or rng[1] > 0):
-                if any(_parallel_k_race(sec, name) for sec in vl.sections):
-                    raise UnsupportedStencil(f"'{name}' written and read at a K offset in one PARALLEL loop")
+        tail = self.tail
+        tail_write = tail.fields if (tail is not None and tail.a == li) else []
+        tail_read = set(tail.fields) if (tail is not None and tail.b == li) else set()
+        no_store = tail.no_store if (tail is not None and tail.a == li) else set()
         decl_dtype = {}
         for (name, di, dj) in win:
             decl_dtype[name] = self.st.decl(name).dtype
@@ -206,25 +357,32 @@ class ColumnGen:
 
         def mem_ptr(name, di, dj, kexpr):
             c = cname(name)
-            return (
-                f"p.p_{c} + ((int64_t)gtmi::clampi(i + ({di}), p.ilo_{c}, p.ihi_{c}) * p.sI_{c} + "
-                f"(int64_t)gtmi::clampi(j + ({dj}), p.jlo_{c}, p.jhi_{c}) * p.sJ_{c} + "
-                f"(int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
-            )
+            return f"({self.bases[(name, di, dj)]} + (int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
 
         def mem_index(name, di, dj, kexpr):
             """A load expression (non-temporal for read-once streams)."""
             nt = "true" if (name in self.nt_loads and name not in direct) else "false"
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
 
+        def load_into(var, name, di, dj, kexpr, maybe_cached=True) -> List[str]:
+            """``var = F(level kexpr)``: from the LDS tail cache when this loop reads a cached level
+            (a run-time test unless ``maybe_cached`` is False: the level is known not to be cached)."""
+            if maybe_cached and name in tail_read and (di, dj) == (0, 0):
+                return [
+                    f"{{ const int lv_ = {kexpr};",
+                    f"  if (lv_ >= tc0 && lv_ < tc1) {var} = {tail.var(name)}[(lv_ - tc0) * 256 + tid];",
+                    f"  else {var} = {mem_index(name, di, dj, 'lv_')}; }}",
+                ]
+            return [f"{var} = {mem_index(name, di, dj, kexpr)};"]
+
         def mem_store(name, kexpr, value):
             nt = "true" if (name in self.nt_stores and name not in direct) else "false"
-            return f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
+            st = f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
+            if name in no_store and kexpr == "k":
+                st = f"if (k < tc0 || k >= tc1) {st}"
+            return st
 
-        P = int(self.opts.get("kprefetch", 0))
-        U = int(self.opts.get("kblock", 0))
-        if U > 1:
-            P = 0  # blocked loads replace the rotating prefetch registers
+        P = self.ring
         step = "+" if fwd else "-"
         out = [f"{{  // vertical loop {li} ({order.name})"]
         for (name, di, dj), rng in win.items():
@@ -261,12 +419,15 @@ class ColumnGen:
                 front_load[key] = any(zero_needed_in(name, di, dj, sec) for sec in vl.sections)
             else:
                 front_load[key] = True
-        # prefetch registers: front values of the next P levels
-        for key, fl in front_load.items():
-            if fl:
-                t = decl_dtype[key[0]].ctype
-                for pp in range(1, P + 1):
-                    out.append(f"    {t} pf{pp}_{wvar(*key, front[key])} = ({t})0;")
+        # ring keys: every loaded front, except fields this loop writes that have no K axis (IJ
+        # temporaries/fields: every level is the same address, so a front fetched ahead would
+        # miss the writes of the levels in between)
+        ring_keys = [
+            key for key, fl in front_load.items()
+            if fl and not (key[0] in wnames and "K" not in self.st.decl(key[0]).axes)
+        ] if P > 1 else []
+        # fronts of tail-cached fields in the reading loop (LDS source in the cached segment)
+        tail_keys = [key for key, fl in front_load.items() if fl and key[0] in tail_read and key[1:] == (0, 0)]
 
         for si, sec in enumerate(vl.sections):
             lo, hi = interval_bounds(sec.interval)
@@ -289,95 +450,166 @@ class ColumnGen:
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
             self._kaddr = kaddr
 
-            def level_body(u: Optional[int]) -> List[str]:
-                """One level: window (re)load or shift, then the statements. ``u``: the level's
-                slot in a block of ``U`` levels whose window fronts were loaded together."""
-                body = ["if (k != k_next) {  // (re)load the full K-window and the prefetch registers"]
+            def shift_and_fronts(slot: Optional[int], mode: str) -> List[str]:
+                """Shift every window one level and load each front: from ring ``slot``, from the
+                LDS tail cache (``mode`` "lds"), or from memory here (``slot`` None)."""
+                body = []
+                for key, rng in win.items():
+                    name, di, dj = key
+                    ds = list(range(rng[0], rng[1] + 1))
+                    if fwd:
+                        for d in ds[:-1]:
+                            body.append(f"{wvar(name, di, dj, d)} = {wvar(name, di, dj, d + 1)};")
+                    else:
+                        for d in reversed(ds[1:]):
+                            body.append(f"{wvar(name, di, dj, d)} = {wvar(name, di, dj, d - 1)};")
+                    if front_load[key]:
+                        fd = front[key]
+                        fv = wvar(name, di, dj, fd)
+                        if mode == "lds" and key in tail_keys:
+                            body.append(f"{fv} = {tail.var(name)}[(k + ({fd}) - tc0) * 256 + tid];")
+                        elif slot is not None and key in ring_keys:
+                            body.append(f"{fv} = rg{slot}_{fv};")
+                        else:
+                            body += load_into(fv, name, di, dj, f"k + ({fd})", maybe_cached=(mode == "mixed"))
+                return body
+
+            def reload() -> List[str]:
+                body = []
                 for (name, di, dj), rng in win.items():
                     if not self._mem(name):
                         continue
                     for d in range(rng[0], rng[1] + 1):
                         if d == 0 and not zero_needed_in(name, di, dj, sec):
                             continue
-                        body.append(f"    {wvar(name, di, dj, d)} = {mem_index(name, di, dj, f'k + ({d})')};")
-                for key, fl in front_load.items():
-                    if fl:
-                        fd = front[key]
-                        for pp in range(1, P + 1):
-                            body.append(
-                                f"    pf{pp}_{wvar(*key, fd)} = {mem_index(*key, f'k {step} {pp} + ({fd})')};"
-                            )
-                body.append("} else {  // shift the window; its front comes from the prefetch registers")
-                for key, rng in win.items():
-                    name, di, dj = key
-                    ds = list(range(rng[0], rng[1] + 1))
-                    if fwd:
-                        for d in ds[:-1]:
-                            body.append(f"    {wvar(name, di, dj, d)} = {wvar(name, di, dj, d + 1)};")
-                    else:
-                        for d in reversed(ds[1:]):
-                            body.append(f"    {wvar(name, di, dj, d)} = {wvar(name, di, dj, d - 1)};")
-                    if front_load[key]:
-                        fd = front[key]
-                        fv = wvar(name, di, dj, fd)
-                        if u is not None:
-                            body.append(f"    {fv} = bf{u}_{fv};")
-                        elif P == 0:
-                            body.append(f"    {fv} = {mem_index(name, di, dj, f'k + ({fd})')};")
-                        else:
-                            body.append(f"    {fv} = pf1_{fv};")
-                            for pp in range(1, P):
-                                body.append(f"    pf{pp}_{fv} = pf{pp + 1}_{fv};")
-                            body.append(f"    pf{P}_{fv} = {mem_index(name, di, dj, f'k {step} {P} + ({fd})')};")
-                body.append("}")
-                body.append(f"k_next = k {step} 1;")
+                        body += load_into(wvar(name, di, dj, d), name, di, dj, f"k + ({d})")
+                return body
+
+            def statements() -> List[str]:
+                body = [f"k_next = k {step} 1;"]
                 for ti, s in enumerate(sec.body):
                     code = self._stmt(s, rend, wvar, mem_store)
                     g = self._guard(li, si, ti)
                     if g:
                         code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
                     body += code
+                if tail_write:
+                    body.append("if (k >= tc0 && k < tc1) {  // LDS tail cache: this level's final values")
+                    for n in tail_write:
+                        body.append(f"    {tail.var(n)}[(k - tc0) * 256 + tid] = {wvar(n, 0, 0, 0)};")
+                    body.append("}")
                 return body
 
-            if U > 1:
-                # blocked K loads: the window fronts of U levels are issued together (U independent
-                # loads per stream in flight per wave), then the U levels are computed in order;
-                # levels past the section end re-read its last level (a cache hit, no extra HBM bytes)
+            def entry_level(slot, mode) -> List[str]:
+                """A segment's first level, which may follow a gap: full window reload unless it
+                continues the sweep (the only level with loads inside a branch)."""
+                return (["if (k != k_next) {  // (re)load the full K-window"] + ["    " + x for x in reload()]
+                        + ["} else {"] + ["    " + x for x in shift_and_fronts(slot, mode)] + ["}"]
+                        + statements())
+
+            def refill(slot, R, keys) -> List[str]:
+                body = []
+                for key in keys:
+                    fv = wvar(*key, front[key])
+                    body += load_into(f"rg{slot}_{fv}", *key, f"k {step} {R} + ({front[key]})", maybe_cached=False)
+                return body
+
+            def segment(ss, se, mode: str) -> List[str]:
+                """Levels [ss, se) of the section in sweep order. ``mode``: "mem" (no front of
+                these levels is tail-cached), "lds" (every tail-cached front is), "mixed"."""
+                keys = [k_ for k_ in ring_keys if not (mode == "lds" and k_ in tail_keys)] if mode != "mixed" else []
+                R = _section_ring(sec.interval, P) if keys else 0
+                o = [f"{{  // levels [{ss}, {se}), {mode}"]
+                o.append(f"    const int ss = {ss}, se = {se};")
+                first = "ss" if fwd else "se - 1"
+                o.append("    if (ss < se) {")
+                if R <= 1:
+                    # no ring: fronts loaded at their level (first level peeled: the loop itself has
+                    # no branch around a load)
+                    o.append("        {")
+                    o.append(f"            const int k = {first};")
+                    o += ["            " + x for x in entry_level(None, mode)]
+                    o.append("        }")
+                    if fwd:
+                        o.append("        for (int k = ss + 1; k < se; ++k) {")
+                    else:
+                        o.append("        for (int k = se - 2; k >= ss; --k) {")
+                    o += ["            " + x for x in shift_and_fronts(None, mode) + statements()]
+                    o.append("        }")
+                    o.append("    }")
+                    o.append("}")
+                    return o
+                for u in range(R):
+                    for key in keys:
+                        fv = wvar(*key, front[key])
+                        t = decl_dtype[key[0]].ctype
+                        o.append(f"        {t} rg{u}_{fv};")
+                        o += ["        " + x for x in load_into(f"rg{u}_{fv}", *key, f"{first} {step} {u} + ({front[key]})",
+                                                                maybe_cached=False)]
+                # first level: reload or continue; ring slot 0
+                o.append("        {")
+                o.append(f"            const int k = {first};")
+                o += ["            " + x for x in entry_level(0, mode)]
+                o += ["            " + x for x in refill(0, R, keys)]
+                o.append("        }")
+                # full blocks of R levels: shift only, no branches around loads (a load inside a
+                # branch makes the compiler drain every load in flight at the join)
                 if fwd:
-                    out.append(f"        for (int kb = ks; kb < ke; kb += {U}) {{")
+                    o.append("        int kb = ss + 1;")
+                    o.append(f"        for (; kb + {R - 1} < se; kb += {R}) {{")
                 else:
-                    out.append(f"        for (int kb = ke - 1; kb >= ks; kb -= {U}) {{")
-                for key, fl in front_load.items():
-                    if not fl:
-                        continue
-                    fd = front[key]
-                    fv = wvar(*key, fd)
-                    t = decl_dtype[key[0]].ctype
-                    for u in range(U):
-                        kl = f"min(kb + {u}, ke - 1)" if fwd else f"max(kb - {u}, ks)"
-                        out.append(f"            const {t} bf{u}_{fv} = {mem_index(*key, f'{kl} + ({fd})')};")
-                for u in range(U):
-                    cond = f"k < ke" if fwd else "k >= ks"
-                    out.append(f"            {{  // level kb {step} {u}")
-                    out.append(f"                const int k = kb {step} {u};")
-                    out.append(f"                if ({cond}) {{")
-                    out += ["                    " + x for x in level_body(u)]
-                    out.append("                }")
-                    out.append("            }")
-                out.append("        }")
+                    o.append("        int kb = se - 2;")
+                    o.append(f"        for (; kb - {R - 1} >= ss; kb -= {R}) {{")
+                for u in range(R):
+                    slot = (u + 1) % R
+                    o.append(f"            {{  // ring slot {slot}")
+                    o.append(f"                const int k = kb {step} {u};")
+                    o += ["                " + x for x in shift_and_fronts(slot, mode) + statements()
+                          + refill(slot, R, keys)]
+                    o.append("            }")
+                o.append("        }")
+                # the last < R levels: their fronts are already in the ring
+                for u in range(R - 1):
+                    slot = (u + 1) % R
+                    cond = f"kb + {u} < se" if fwd else f"kb - {u} >= ss"
+                    o.append(f"        if ({cond}) {{  // ring slot {slot}")
+                    o.append(f"            const int k = kb {step} {u};")
+                    o += ["            " + x for x in shift_and_fronts(slot, mode) + statements()]
+                    o.append("        }")
+                o.append("    }")
+                o.append("}")
+                return o
+
+            if tail_keys:
+                # split the section by where the tail-cached fronts come from. A front k + fd is
+                # cached iff tc0 <= k + fd < tc1. With lo/hi the smallest/largest fd of the tail keys:
+                # all fronts cached for k in [tc0 - lo, tc1 - hi), none below tc0 - hi or from
+                # tc1 - lo on. Levels before the cached band in sweep order are run "mixed" (their
+                # ring would look ahead into the cache); the band itself reads LDS; the levels after
+                # it stream from memory with the ring.
+                fds = [front[k_] for k_ in tail_keys]
+                lo_fd, hi_fd = min(fds), max(fds)
+                mn = lambda a, b: f"({a} < {b} ? {a} : {b})"  # noqa: E731
+                mx = lambda a, b: f"({a} > {b} ? {a} : {b})"  # noqa: E731
+                out.append(f"        const int x1 = tc0 - ({hi_fd}), x2 = {mx('x1', f'tc0 - ({lo_fd})')};")
+                out.append(f"        const int x3 = {mx('x2', f'tc1 - ({hi_fd})')}, x4 = tc1 - ({lo_fd});  // x1 <= x2 <= x3 <= x4")
+                x1, x2, x3, x4 = "x1", "x2", "x3", "x4"
+                rng_ = lambda a, b: (mx("ks", a) if a else "ks", mn("ke", b) if b else "ke")  # noqa: E731
+                if fwd:
+                    parts = [(*rng_(None, x2), "mixed"), (*rng_(x2, x3), "lds"), (*rng_(x3, x4), "mixed"),
+                             (*rng_(x4, None), "mem")]
+                else:
+                    parts = [(*rng_(x3, None), "mixed"), (*rng_(x2, x3), "lds"), (*rng_(x1, x2), "mixed"),
+                             (*rng_(None, x1), "mem")]
+                for ss, se, mode in parts:
+                    out += ["        " + x for x in segment(ss, se, mode)]
             else:
-                if fwd:
-                    out.append("        for (int k = ks; k < ke; ++k) {")
-                else:
-                    out.append("        for (int k = ke - 1; k >= ks; --k) {")
-                out += ["            " + x for x in level_body(None)]
-                out.append("        }")
+                out += ["        " + x for x in segment("ks", "ke", "mem")]
             out.append("    }")
         out.append("}")
         return out
 
     def _stmt(self, s, rend, wvar, mem_store) -> List[str]:
-        mem_index = mem_store
         if isinstance(s, ir.Assign):
             name = s.target.name
             if name in self.direct:
@@ -396,27 +628,61 @@ class ColumnGen:
         if isinstance(s, ir.If):
             out = [f"if ({rend(s.cond)}) {{"]
             for x in s.body:
-                out += ["    " + y for y in self._stmt(x, rend, wvar, mem_index)]
+                out += ["    " + y for y in self._stmt(x, rend, wvar, mem_store)]
             if s.orelse:
                 out.append("} else {")
                 for x in s.orelse:
-                    out += ["    " + y for y in self._stmt(x, rend, wvar, mem_index)]
+                    out += ["    " + y for y in self._stmt(x, rend, wvar, mem_store)]
             out.append("}")
             return out
         if isinstance(s, ir.While):
             out = [f"while ({rend(s.cond)}) {{"]
             for x in s.body:
-                out += ["    " + y for y in self._stmt(x, rend, wvar, mem_index)]
+                out += ["    " + y for y in self._stmt(x, rend, wvar, mem_store)]
             out.append("}")
             return out
         if isinstance(s, ir.HorizontalRegion):
             cond = region_condition(s.masks, "i", "j", "p.ni", "p.nj")
             out = [f"if ({cond}) {{"]
             for x in s.body:
-                out += ["    " + y for y in self._stmt(x, rend, wvar, mem_index)]
+                out += ["    " + y for y in self._stmt(x, rend, wvar, mem_store)]
             out.append("}")
             return out
         raise TypeError(type(s))
+
+
+def _bound_eq(a: ir.AxisBound, b: ir.AxisBound) -> bool:
+    return a.level == b.level and a.offset == b.offset
+
+
+def _contiguous(vl: ir.VerticalLoop) -> bool:
+    """Consecutive sections (in sweep order) share their boundary: no level is skipped between them."""
+    secs = vl.sections
+    fwd = vl.loop_order != ir.LoopOrder.BACKWARD
+    for s0, s1 in zip(secs, secs[1:]):
+        if fwd and not _bound_eq(s0.interval.end, s1.interval.start):
+            return False
+        if not fwd and not _bound_eq(s0.interval.start, s1.interval.end):
+            return False
+    return True
+
+
+def _covers_all_levels(vl: ir.VerticalLoop, fwd: bool) -> bool:
+    """The loop's sections run every level of [0, nk) exactly once (statically provable)."""
+    if not vl.sections or not _contiguous(vl):
+        return False
+    first, last = vl.sections[0].interval, vl.sections[-1].interval
+    lo = first.start if fwd else last.start
+    hi = last.end if fwd else first.end
+    return _bound_eq(lo, ir.AxisBound(ir.LevelMarker.START, 0)) and _bound_eq(hi, ir.AxisBound(ir.LevelMarker.END, 0))
+
+
+def _section_ring(itv: ir.Interval, P: int) -> int:
+    """Ring depth of a section: ``P``, or its static length when that is shorter (a one-level
+    section such as ``interval(0, 1)`` loads its fronts directly)."""
+    if itv.start.level == itv.end.level:
+        return max(0, min(P, itv.end.offset - itv.start.offset))
+    return P
 
 
 def _parallel_k_race(sec: ir.Section, name: str) -> bool:
