@@ -28,7 +28,7 @@ import dataclasses
 from typing import Dict, List, Optional, Set, Tuple
 
 from gt4py_amd import ir
-from gt4py_amd.codegen.plan import ColumnKernel, KernelPlan, UnsupportedStencil
+from gt4py_amd.codegen.plan import ColumnKernel, KernelPlan, UnsupportedStencil, sections_contiguous
 from gt4py_amd.passes import StencilAnalysis, iter_accesses
 from gt4py_amd.codegen.common import (  # noqa: F401
     COLUMN_BLOCK, ExprRenderer, FieldSlot, cname, host_fill, interval_bounds, kparam_decl, region_condition,
@@ -141,8 +141,8 @@ class ColumnGen:
                 if any(_parallel_k_race(sec, name) for sec in vl.sections):
                     raise UnsupportedStencil(f"'{name}' written and read at a K offset in one PARALLEL loop")
             if not self._mem(name) and rng[0] != rng[1] and not _contiguous(vl):
-                # a register-only value read at another level across a gap between sections: the
-                # gap levels never run, so the window cannot carry it (staged lowering puts it in scratch)
+                # the planner puts such temporaries in scratch (plan.make_plan); a register window
+                # cannot carry a value across levels that never run
                 raise UnsupportedStencil(f"register temporary '{name}' read at a K offset across a section gap")
         return _LoopInfo(vl.loop_order != ir.LoopOrder.BACKWARD, direct, win, wnames)
 
@@ -655,16 +655,7 @@ def _bound_eq(a: ir.AxisBound, b: ir.AxisBound) -> bool:
     return a.level == b.level and a.offset == b.offset
 
 
-def _contiguous(vl: ir.VerticalLoop) -> bool:
-    """Consecutive sections (in sweep order) share their boundary: no level is skipped between them."""
-    secs = vl.sections
-    fwd = vl.loop_order != ir.LoopOrder.BACKWARD
-    for s0, s1 in zip(secs, secs[1:]):
-        if fwd and not _bound_eq(s0.interval.end, s1.interval.start):
-            return False
-        if not fwd and not _bound_eq(s0.interval.start, s1.interval.end):
-            return False
-    return True
+_contiguous = sections_contiguous
 
 
 def _covers_all_levels(vl: ir.VerticalLoop, fwd: bool) -> bool:

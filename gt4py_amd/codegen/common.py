@@ -138,6 +138,13 @@ class ExprRenderer:
             return f"gtmi::remainder_(({t}){args[0]}, ({t}){args[1]})"
         if f == "pow":
             if e.dtype.isfloat():
+                ex = e.args[1]
+                while isinstance(ex, ir.Cast):
+                    ex = ex.expr
+                if isinstance(ex, ir.Literal) and float(ex.value) == 2.0:
+                    # x ** 2: glibc's pow (numpy's float power loop) is correctly rounded, so it
+                    # equals the correctly rounded product; ocml's pow is not (1 ULP off)
+                    return f"gtmi::square<{t}>(({t})({args[0]}))"
                 return f"(({t})pow(({t})({args[0]}), ({t})({args[1]})))"
             return f"gtmi::ipow<{t}>(({t})({args[0]}), ({t})({args[1]}))"
         if f in ("isfinite", "isinf", "isnan"):

@@ -82,6 +82,16 @@ def _pointwise_plane_ok(vl: ir.VerticalLoop) -> bool:
     return True
 
 
+def sections_contiguous(vl: ir.VerticalLoop) -> bool:
+    """Consecutive sections (in sweep order) share their boundary: no level is skipped between them."""
+    fwd = vl.loop_order != ir.LoopOrder.BACKWARD
+    for s0, s1 in zip(vl.sections, vl.sections[1:]):
+        a, b = (s0.interval.end, s1.interval.start) if fwd else (s0.interval.start, s1.interval.end)
+        if a.level != b.level or a.offset != b.offset:
+            return False
+    return True
+
+
 def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_plane: bool = False) -> KernelPlan:
     """``column_only``: every computation runs in column kernels (the staged fallback, after
     ``lowering.split_phases``); otherwise PARALLEL computations with horizontal offsets become
@@ -162,11 +172,19 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_pl
                         touch_loops.setdefault(acc.name, set()).add(li)
                         if acc.offset[0] or acc.offset[1]:
                             read_ij_offset.add(acc.name)
+    # a temporary read at a K offset in a loop whose sections leave gaps: the gap levels never run,
+    # so a register window cannot carry the value across them -- it goes through memory
+    gap_read: Set[str] = set()
+    for vl in st.vertical_loops:
+        if not sections_contiguous(vl):
+            for acc, w in _loop_accesses(vl):
+                if not w and isinstance(acc, ir.FieldAccess) and acc.name in temps and acc.offset[2] != 0:
+                    gap_read.add(acc.name)
     scratch = []
     for t in st.temporaries:
         kk = touch_kernels.get(t.name, set())
         ll = touch_loops.get(t.name, set())
-        if len(kk) > 1 or len(ll) > 1:
+        if len(kk) > 1 or len(ll) > 1 or t.name in gap_read:
             scratch.append(t.name)
     # column kernels must not read scratch temporaries written inside the same kernel at IJ offsets
     for k in kernels:

@@ -99,6 +99,8 @@ GTMI_DEV int32_t remainder_(int32_t a, int32_t b) { return remainder_int(a, b); 
 GTMI_DEV int16_t remainder_(int16_t a, int16_t b) { return remainder_int(a, b); }
 GTMI_DEV int8_t remainder_(int8_t a, int8_t b) { return remainder_int(a, b); }
 
+template <typename T> GTMI_DEV T square(T x) { return x * x; }
+
 template <typename T> GTMI_DEV T ipow(T base, T exp) {
     if (exp < 0) return (T)0;  // numpy raises; keep it defined on device
     T r = 1;

@@ -30,6 +30,8 @@ from __future__ import annotations
 import dataclasses
 from typing import Dict, List, Optional, Sequence, Tuple
 
+from gt4py_amd.distributed.halo import halo_fields_read_only
+
 
 def _split(n: int, parts: int, idx: int) -> Tuple[int, int]:
     base, extra = divmod(n, parts)
@@ -253,6 +255,7 @@ class HaloStencil2D:
         self.ni, self.nj = decomp.local_shape(rank)
         self.overlap = (
             overlap and (decomp.size > 1 or force_comm) and self.ni > 2 * self.hi and self.nj > 2 * self.hj
+            and halo_fields_read_only(stencil, self.halo_fields)
         )
         self._stream = None
 

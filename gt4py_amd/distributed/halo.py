@@ -201,7 +201,10 @@ class HaloStencil:
         self.exchange = JHaloExchange(nj_local, halo, rank, world_size, group, periodic, force_comm)
         self.h = halo
         self.nj = nj_local
-        self.overlap = overlap and (world_size > 1 or force_comm) and nj_local > 2 * halo
+        # the overlap packs the halo fields' edge rows while the interior kernel runs: only sound
+        # when the stencil never writes them
+        self.overlap = (overlap and (world_size > 1 or force_comm) and nj_local > 2 * halo
+                        and halo_fields_read_only(stencil, self.halo_fields))
         self._stream = None
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
@@ -244,6 +247,18 @@ class HaloStencil:
             self.exchange.finish(works)
         self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
         self.stencil(**kw, origin=self._shifted(origin, nj - h), domain=(ni, h, nk), validate_args=False)
+
+
+def halo_fields_read_only(stencil, names) -> bool:
+    """Every halo field is only read by ``stencil`` (``field_info`` access kind READ)."""
+    from gt4py_amd.definitions import AccessKind
+
+    info = getattr(stencil, "field_info", None) or {}
+    for n in names:
+        fi = info.get(n)
+        if fi is not None and fi.access & AccessKind.WRITE:
+            return False
+    return True
 
 
 def init_process_group(backend: Optional[str] = None):

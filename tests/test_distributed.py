@@ -268,3 +268,25 @@ def test_jstrips_periodic(tmp_path, world):
     st(gin.copy(), ref, gco, origin={"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)})
     got = np.concatenate([np.load(tmp_path / f"out_{r}.npy") for r in range(world)], axis=1)
     assert np.array_equal(got, ref)
+
+
+def test_overlap_off_when_a_halo_field_is_written():
+    """A stencil that writes one of its halo fields must not overlap the exchange (the packing of
+    that field's edge rows would race with the interior kernel's writes): advisor finding r1."""
+    sys.path.insert(0, REPO)
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed import Decomposition2D, HaloStencil, HaloStencil2D
+    from gt4py_amd.gtscript import PARALLEL, Field, computation, interval
+
+    def smooth(a: Field[np.float64], b: Field[np.float64]):
+        with computation(PARALLEL), interval(...):
+            b = a[0, 1, 0] + a[0, -1, 0]
+
+    st = gtscript.stencil(backend="numpy", definition=smooth, name="dist.readonly")
+    # GTScript forbids reading a written field at IJ offsets, so a written halo field is one the
+    # caller lists although the stencil only writes it ("b")
+    assert HaloStencil(st, ["a"], 16, 1, 0, 2).overlap
+    assert not HaloStencil(st, ["a", "b"], 16, 1, 0, 2).overlap
+    dec = Decomposition2D(16, 16, 2, 1)
+    assert HaloStencil2D(st, ["a"], dec, 0, (1, 1)).overlap
+    assert not HaloStencil2D(st, ["b"], dec, 0, (1, 1)).overlap

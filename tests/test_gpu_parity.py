@@ -91,7 +91,11 @@ def _alloc_fill(shape, dtype, rng, lo, hi, origin):
     return host, storage.from_array(host, None, backend=BACKEND, aligned_index=origin)
 
 
-@pytest.mark.parametrize("dtype,ni,nj,nk", [(np.float64, 2048, 2048, 160), (np.float32, 1024, 1024, 64)])
+@pytest.mark.parametrize(
+    "dtype,ni,nj,nk",
+    # C3 (BASELINE configs[2]); an f32 cast-tree case; C5's per-GPU weak-scaling tile 8192x1024x160 f32
+    [(np.float64, 2048, 2048, 160), (np.float32, 1024, 1024, 64), (np.float32, 8192, 1024, 160)],
+)
 def test_hdiff_full_size_vs_c_oracle(dtype, ni, nj, nk):
     _torch()
     from gt4py_amd import gtscript, storage
