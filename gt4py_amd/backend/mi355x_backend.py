@@ -86,6 +86,7 @@ class Mi355xBackend(BaseBackend):
         "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},
         "kring": {"versioning": True, "type": int, "description": "column kernels: window-front loads in flight (levels)"},
         "ktail_lds": {"versioning": True, "type": int, "description": "column kernels: LDS bytes for the sweep-to-sweep tail cache (0 = off)"},
+        "ktail_all": {"versioning": True, "type": int, "description": "column kernels: tail-cache every eligible field (1) or only write-free scratch when there is any (0)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},

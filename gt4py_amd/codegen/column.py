@@ -178,6 +178,10 @@ class ColumnGen:
                 for n in fields:
                     if n in self.scratch and self._touching_loops(n) <= {la, lb}:
                         no_store.add(n)
+                if no_store and int(self.opts.get("ktail_all", 0)) == 0:
+                    # a cached level of such a field saves its write AND its re-read (twice the HBM
+                    # bytes per LDS byte of a field that is only re-read): give them all the LDS
+                    fields = [n for n in fields if n in no_store]
                 best = _Tail(la, lb, A.fwd, fields, no_store)
         if best is None:
             return None

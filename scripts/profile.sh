@@ -14,12 +14,12 @@ for cfg in ${CONFIGS:-hdiff}; do
   cpu=--no-cpu-baseline
   [ "$cfg" = hdiff ] && cpu=
   echo "== $cfg: bench under kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python3 bench.py --config $cfg --steps 20 --warmup 3 $cpu > $OUT/kt_$cfg.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python3 bench.py --config $cfg --steps 20 --warmup 3 --no-extra $cpu > $OUT/kt_$cfg.log 2>&1 || exit $?
   grep '^{"metric"' $OUT/kt_$cfg.log > $OUT/bench_$cfg.json || exit $?
   cat $OUT/bench_$cfg.json
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg: pmc $c"
-    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${cfg}_$c -o pmc -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_${cfg}_$c.log 2>&1 || exit $?
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${cfg}_$c -o pmc -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-extra > $OUT/pmc_${cfg}_$c.log 2>&1 || exit $?
   done
 done
 find $OUT -name "*.csv" | head -50
