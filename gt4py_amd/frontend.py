@@ -333,7 +333,7 @@ class StencilParser:
             if self._call_name(second) != "interval":
                 raise GTScriptSyntaxError("Expected 'interval(...)' after 'computation(...)'")
             itv = self._parse_interval(second, scope)
-            sections.append(ir.Section(itv, self._parse_block(stmt.body, scope)))
+            sections.append(ir.Section(itv, self._parse_block(stmt.body, scope), 0))
         elif len(items) == 1:
             for sub in stmt.body:
                 if isinstance(sub, ast.Expr) and isinstance(sub.value, ast.Constant):
@@ -341,7 +341,7 @@ class StencilParser:
                 if not (isinstance(sub, ast.With) and self._call_name(sub.items[0].context_expr) == "interval"):
                     raise GTScriptSyntaxError("Inside 'with computation(...)' only 'with interval(...)' blocks")
                 itv = self._parse_interval(sub.items[0].context_expr, scope)
-                sections.append(ir.Section(itv, self._parse_block(sub.body, scope)))
+                sections.append(ir.Section(itv, self._parse_block(sub.body, scope), len(sections)))
         else:
             raise GTScriptSyntaxError("Invalid 'with computation(...)' statement")
 

@@ -334,6 +334,9 @@ class Interval:
 class Section:
     interval: Interval
     body: List[Stmt]
+    # position of the ``with interval`` block in the definition (-1: unknown); sections are
+    # stored in sweep order, the parallel-model rules run in definition order (gtc/gtir.py:226)
+    def_index: int = dataclasses.field(default=-1, compare=False)
 
 
 @dataclasses.dataclass(eq=True)
@@ -430,7 +433,7 @@ def map_expr(node, fn):
     if isinstance(node, HorizontalRegion):
         return HorizontalRegion(node.masks, map_expr(node.body, fn))
     if isinstance(node, Section):
-        return Section(node.interval, map_expr(node.body, fn))
+        return Section(node.interval, map_expr(node.body, fn), node.def_index)
     if isinstance(node, VerticalLoop):
         return VerticalLoop(node.loop_order, [map_expr(s, fn) for s in node.sections])
     raise TypeError(type(node))

@@ -588,7 +588,12 @@ def validate_parallel_model(stencil: ir.Stencil) -> None:
                 raise ValueError(f"Illegal write and read with horizontal offset detected for {names}.")
 
     for vl in stencil.vertical_loops:
-        for sec in vl.sections:
+        secs = list(vl.sections)
+        if all(sec.def_index >= 0 for sec in secs):
+            # the frontend stores sections in sweep order; the temporary a block declares is
+            # decided in definition order, as the reference builds GTIR
+            secs.sort(key=lambda sec: sec.def_index)
+        for sec in secs:
             for s in sec.body:
                 check_stmt(s)
             written = _assign_writes(sec.body)

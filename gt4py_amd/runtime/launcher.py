@@ -25,11 +25,14 @@ _AXES = ("I", "J", "K")
 _NEVER = object()
 
 
-def _data_ptr(a):
-    dp = getattr(a, "data_ptr", None)
-    if dp is not None:
-        return dp()
-    return a.__cuda_array_interface__["data"][0]
+def _layout(a):
+    """(data pointer, shape, strides) of a device array: a cached pack is reused only when all
+    three still match (a tensor changed in place by set_/resize_/as_strided_ keeps its identity)."""
+    st = getattr(a, "stride", None)
+    if st is not None:
+        return a.data_ptr(), tuple(a.shape), tuple(st())
+    cai = a.__cuda_array_interface__
+    return cai["data"][0], tuple(cai["shape"]), tuple(cai.get("strides") or ())
 
 
 def device_tensor(obj):
@@ -101,8 +104,8 @@ class StencilLauncher:
         """The ``gtmi_field`` array for a call (+ the device), cached per (arrays, origins, domain).
 
         A repeated call with the same tensor objects, origins and domain reuses the packed structs:
-        the entry holds weak references to the arrays and their data pointers, so a freed or
-        re-allocated tensor never matches a stale entry.
+        the entry holds weak references to the arrays and their data pointers, shapes and strides,
+        so a freed, re-allocated or re-strided tensor never matches a stale entry.
         """
         lib = self.lib  # noqa: F841  (loads the signature)
         key = (tuple(domain),) + tuple(
@@ -114,7 +117,7 @@ class StencilLauncher:
             ok = True
             for d, r, p in zip(self.fields, refs, ptrs):
                 a = arrays.get(d["name"])
-                if (r is None) != (a is None) or (r is not None and (r() is not a or _data_ptr(a) != p)):
+                if (r is None) != (a is None) or (r is not None and (r() is not a or _layout(a) != p)):
                     ok = False
                     break
             if ok:
@@ -146,7 +149,7 @@ class StencilLauncher:
                 refs.append(weakref.ref(arr))
             except TypeError:  # not weak-referenceable: never reuse this entry
                 refs.append(lambda: _NEVER)
-            ptrs.append(t.data_ptr())
+            ptrs.append(_layout(arr))
             device = t.device
             want = np.dtype(decl["dtype"])
             got = _np_dtype_of(t)

@@ -206,6 +206,36 @@ def test_no_write_and_read_with_horizontal_offset(backend):
 
 
 @pytest.mark.parametrize("backend", BUILD_BACKENDS)
+def test_temporary_declared_in_definition_order(backend):
+    """A temporary belongs to the interval block that assigns it FIRST IN THE DEFINITION
+    (gtc/gtir.py:226-240: each block is a GTIR VerticalLoop with its own ``temporaries``),
+    not to the block that comes first in the sweep: here ``tmp`` is declared by the upper block,
+    so the lower block, defined later, writes it and reads it at an I offset -- rejected."""
+    with pytest.raises(ValueError, match="Illegal write and read with horizontal offset"):
+
+        @gtscript.stencil(backend=backend)
+        def declared_later(a: Field[np.float64], b: Field[np.float64]) -> None:
+            with computation(PARALLEL):
+                with interval(1, None):
+                    tmp = a * 2
+                    b = tmp
+                with interval(0, 1):
+                    tmp = a
+                    b = tmp[1, 0, 0]
+
+    # defined the other way round the lower block declares tmp and may read it at an offset
+    @gtscript.stencil(backend=backend)
+    def declared_first(a: Field[np.float64], b: Field[np.float64]) -> None:
+        with computation(PARALLEL):
+            with interval(0, 1):
+                tmp = a
+                b = tmp[1, 0, 0]
+            with interval(1, None):
+                tmp = a * 2
+                b = tmp
+
+
+@pytest.mark.parametrize("backend", BUILD_BACKENDS)
 def test_k_offsets_in_parallel_loops(backend):
     """REF:1660-1720 -- writes and K-offset reads of one field in a PARALLEL loop."""
     with pytest.raises(ValueError, match="write and read with k-offsets in PARALLEL"):
