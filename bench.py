@@ -360,7 +360,11 @@ class Workload:
         if self.halo is not None:
             self.halo(self.named, self.origin, self.domain)
         else:
-            self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain, validate_args=False)
+            self.plain_step()
+
+    def plain_step(self):
+        """One launch over the whole local domain, no exchange (the halo path's A/B reference)."""
+        self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain, validate_args=False)
 
     def library_key(self):
         """Content key of the generated library (``.gt_cache/gt_mi355x/<key>/stencil.so``)."""
@@ -370,15 +374,16 @@ class Workload:
         return os.path.basename(os.path.dirname(compiled.lib_path))
 
 
-def time_workload(wl, steps, warmup, dev, dist=None, events=True):
+def time_workload(wl, steps, warmup, dev, dist=None, events=True, step=None):
     """W untimed warm-ups, then K steps bracketed by barrier + synchronize; returns (elapsed s,
     mean per-launch kernel ms from HIP events on the launch stream, or None)."""
     import torch
 
     cuda = dev.type == "cuda"
     sync = torch.cuda.synchronize if cuda else (lambda: None)
+    step = step or wl.step
     for _ in range(warmup):
-        wl.step()
+        step()
     sync()
     if dist is not None:
         dist.barrier()
@@ -391,9 +396,10 @@ def time_workload(wl, steps, warmup, dev, dist=None, events=True):
     for s in range(steps):
         if evs is not None:
             evs[s][0].record()
-        wl.step()
+        step()
         if evs is not None:
             evs[s][1].record()
+    wl.enqueue_s = time.perf_counter() - t0  # host time to enqueue the K steps (before the final sync)
     sync()
     if dist is not None:
         dist.barrier()
@@ -551,6 +557,17 @@ def main():
         t = torch.tensor([elapsed, kernel_ms or 0.0], device=tdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), (float(t[1]) if kernel_ms is not None else None)
+    halo_ab = None
+    if args.halo_selfcomm and world == 1:
+        # A/B on the same buffers in the same process: whole-domain launch without exchange,
+        # interleaved with a second halo-path measurement
+        el_p, km_p = time_workload(wl, args.steps, args.warmup, dev, dist, step=wl.plain_step)
+        el_h, _ = time_workload(wl, args.steps, args.warmup, dev, dist)
+        enq = wl.enqueue_s
+        halo_ab = {"plain_ms_per_step": round(el_p / args.steps * 1e3, 4), "plain_kernel_ms": round(km_p, 4),
+                   "halo_host_enqueue_ms_per_step": round(enq / args.steps * 1e3, 4),
+                   "halo_ms_per_step": round(min(elapsed, el_h) / args.steps * 1e3, 4),
+                   "overhead": round(min(elapsed, el_h) / el_p - 1.0, 4)}
     ni, nj, nk = wl.domain
     cells_per_step = ni * nj * nk
     total_cells = wl.global_ij[0] * wl.global_ij[1] * nk * args.steps
@@ -602,6 +619,8 @@ def main():
             "library": key,
         },
     }
+    if halo_ab is not None:
+        result["halo_ab"] = halo_ab
     if args.dry_run:
         result["dry_run"] = True
         result["data"] = "synthetic; DRY RUN on CPU (numpy backend, gloo): not a measurement"

@@ -19,15 +19,17 @@ Periodic boundaries (optional per axis) wrap the neighbour ranks; a periodic axi
 rank copies its own opposite face. Non-periodic global boundaries keep the caller's halo cells
 (plain input, as in the reference).
 
-Overlap: packing, the transfers and unpacking run on a dedicated HIP stream (RCCL orders its
-work after the current stream at call time), while the interior, which reads no halo, is
-computed on the caller's stream; the four boundary bands run after the compute stream waits
-on the halo stream.
+Overlap (default, ``GTMI_HALO_STREAM=side``): both phases run on a high-priority halo stream
+(its own hardware queue, ``halo.rccl_options``) while the interior, which reads no halo, runs on
+the caller's stream; the four boundary bands follow once the caller's stream waits on the halo
+stream. ``main``: phase 1 is packed on the caller's stream and handed to RCCL, the interior runs
+while the I faces move, then phase 2 and the bands follow on the caller's stream.
 """
 
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from gt4py_amd.distributed.halo import halo_fields_read_only
@@ -146,12 +148,16 @@ class HaloExchange2D:
         return self._bufs[key][:numel]
 
     def _phase(self, fields: Sequence, phase: int) -> None:
+        self._phase_finish(self._phase_start(fields, phase))
+
+    def _phase_start(self, fields: Sequence, phase: int):
+        """Pack the phase's faces and post its transfers; returns the state ``_phase_finish`` needs."""
         import torch.distributed as dist
 
         faces = self._faces(phase)
         dirs = [d for d in faces if self.nbr[d] is not None]
         if not dirs:
-            return
+            return None
         sizes = {d: [t[faces[d][0][0], faces[d][0][1], :].numel() for t in fields] for d in dirs}
         sbuf, rbuf = {}, {}
         for d in dirs:
@@ -187,10 +193,17 @@ class HaloExchange2D:
             gpeer = dist.get_global_rank(self.group, peer) if self.group is not None else peer
             ops.append(dist.P2POp(dist.irecv, rbuf[d], gpeer, self.group))
             unpack.append((d, rbuf[d]))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-        if device:
+        works = dist.batch_isend_irecv(ops) if ops else []
+        return fields, faces, sizes, rbuf, unpack, works, (unpack_dev if device else None)
+
+    def _phase_finish(self, state) -> None:
+        """Wait for the phase's transfers and unpack the received faces."""
+        if state is None:
+            return
+        fields, faces, sizes, rbuf, unpack, works, unpack_dev = state
+        for w in works:
+            w.wait()
+        if unpack_dev is not None:
             for d, buf in unpack:
                 if buf is not rbuf[d]:  # local periodic wrap: my own opposite face
                     rbuf[d].copy_(buf)
@@ -225,16 +238,32 @@ class HaloExchange2D:
             self._copies[key] = (BatchedCopy(pack), BatchedCopy(unpack))
         return self._copies[key]
 
+    def _groups(self, fields):
+        if self._host is None:
+            self._host = _backend_name(self.group) == "gloo"
+        dtypes = []
+        for t in fields:
+            if t.dtype not in dtypes:
+                dtypes.append(t.dtype)
+        return [[t for t in fields if t.dtype == dt] for dt in dtypes]  # one batched message per neighbour and dtype
+
     def exchange(self, fields: Sequence) -> None:
         """Fill the halos (and corners) of ``fields``; must be called by every rank."""
         if not fields:
             return
-        if self._host is None:
-            self._host = _backend_name(self.group) == "gloo"
-        dtypes = {t.dtype for t in fields}
-        for dt in dtypes:  # one batched message per neighbour and dtype
-            group = [t for t in fields if t.dtype == dt]
+        for group in self._groups(fields):
             self._phase(group, 0)
+            self._phase(group, 1)
+
+    def start(self, fields: Sequence):
+        """Post phase 0 (I faces) of every dtype group; ``finish`` completes both phases."""
+        if not fields:
+            return []
+        return [(group, self._phase_start(group, 0)) for group in self._groups(fields)]
+
+    def finish(self, pending) -> None:
+        for group, state in pending:
+            self._phase_finish(state)
             self._phase(group, 1)
 
 
@@ -258,6 +287,7 @@ class HaloStencil2D:
             and halo_fields_read_only(stencil, self.halo_fields)
         )
         self._stream = None
+        self.stream_mode = os.environ.get("GTMI_HALO_STREAM", "side")
 
     def _run(self, kw, origin, i0, j0, ni, nj, nk):
         if ni <= 0 or nj <= 0:
@@ -288,11 +318,11 @@ class HaloStencil2D:
             return
         hi, hj = self.hi, self.hj
         on_gpu = fields and getattr(fields[0], "is_cuda", False) and not _backend_name(self.ex.group) == "gloo"
-        if on_gpu:
+        if on_gpu and self.stream_mode == "side":
             import torch
 
             if self._stream is None:
-                self._stream = torch.cuda.Stream(device=fields[0].device)
+                self._stream = torch.cuda.Stream(device=fields[0].device, priority=-1)
             main = torch.cuda.current_stream(fields[0].device)
             self._stream.wait_stream(main)  # the fields' producers
             with torch.cuda.stream(self._stream):
@@ -300,7 +330,10 @@ class HaloStencil2D:
             self._run(kw, origin, hi, hj, ni - 2 * hi, nj - 2 * hj, nk)
             main.wait_stream(self._stream)
         else:
-            self.ex.exchange(fields)
+            # default: phase 0 (I faces) is packed and posted on the caller's stream, the interior
+            # runs while RCCL moves it; phase 1 (J faces incl. the received I halos) follows
+            pending = self.ex.start(fields)
             self._run(kw, origin, hi, hj, ni - 2 * hi, nj - 2 * hj, nk)
+            self.ex.finish(pending)
         for i0, j0, bi, bj in self.bands():
             self._run(kw, origin, i0, j0, bi, bj, nk)

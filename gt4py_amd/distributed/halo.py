@@ -14,13 +14,14 @@ per neighbour -- there are no reductions, so no ring collective is involved.
 Global boundaries are plain input cells (no periodicity, as in the reference).
 
 ``HaloStencil`` overlaps the exchange with compute: the rows that do not read the halo run
-while RCCL moves the faces (RCCL's own stream waits on the packing copies; the compute stream
+while RCCL moves the faces (RCCL's own stream waits on the packing kernel; the compute stream
 waits on the transfers only before unpacking), then the two boundary strips run.
 """
 
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 
@@ -206,6 +207,7 @@ class HaloStencil:
         self.overlap = (overlap and (world_size > 1 or force_comm) and nj_local > 2 * halo
                         and halo_fields_read_only(stencil, self.halo_fields))
         self._stream = None
+        self.stream_mode = os.environ.get("GTMI_HALO_STREAM", "side")
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
@@ -223,26 +225,33 @@ class HaloStencil:
             return
         h = self.h
         on_gpu = bool(fields) and getattr(fields[0], "is_cuda", False) and _backend_name(self.exchange.group) != "gloo"
-        if on_gpu:
-            # the interior (rows [h, nj-h): reads no halo) is enqueued FIRST on the compute stream,
-            # so the host cost of posting the RCCL work is hidden behind it; packing, transfers
-            # and unpacking run on the halo stream (after the fields' producers), then the two
-            # boundary strips follow on the compute stream.
+        if on_gpu and self.stream_mode == "side":
+            # default on the GPU: pack -> RCCL -> unpack on a HIGH-priority halo stream (never the
+            # caller's hardware queue, see rccl_options), queued BEFORE the interior so that the
+            # transfer is posted first; the interior (rows [h, nj - h)) runs on the caller's
+            # stream meanwhile, the two boundary strips after it waits on the halo stream.
+            # Measured per-rank cost (rank = own periodic neighbour): +2.2 % vs
+            # +2.5 % for the caller's-stream ordering ("main") and +3.0 % for no overlap.
             import torch
 
             dev = fields[0].device
             if self._stream is None:
-                self._stream = torch.cuda.Stream(device=dev)
+                self._stream = torch.cuda.Stream(device=dev, priority=-1)
             main = torch.cuda.current_stream(dev)
             ready = main.record_event()
-            self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
             self._stream.wait_event(ready)
             with torch.cuda.stream(self._stream):
-                self.exchange.finish(self.exchange.start(fields))
+                works = self.exchange.start(fields)
+            # the transfers are posted before the interior is enqueued
+            self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
+            with torch.cuda.stream(self._stream):
+                self.exchange.finish(works)
             main.wait_stream(self._stream)
         else:
+            # "main" (and the CPU/gloo path): pack on the caller's stream, post the transfers
+            # (RCCL's stream waits on the pack), enqueue the interior (rows [h, nj - h): reads rows
+            # [0, nj) of the halo'ed fields only), then wait on the transfers and unpack
             works = self.exchange.start(fields)
-            # interior rows [h, nj - h): read rows [0, nj) of the halo'ed fields only
             self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
             self.exchange.finish(works)
         self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
@@ -261,6 +270,18 @@ def halo_fields_read_only(stencil, names) -> bool:
     return True
 
 
+def rccl_options():
+    """ProcessGroupNCCL options for the halo exchange: RCCL on HIGH-priority streams. HIP pools
+    hardware queues per priority (GPU_MAX_HW_QUEUES = 4 per process), so a high-priority RCCL
+    stream never shares an in-order hardware queue with the caller's compute stream -- sharing
+    one serialises the transfer behind (or ahead of) the interior kernel."""
+    import torch.distributed as dist
+
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
+
+
 def init_process_group(backend: Optional[str] = None):
     """Initialise torch.distributed from the torchrun environment (127.0.0.1 rendezvous)."""
     import os
@@ -276,7 +297,7 @@ def init_process_group(backend: Optional[str] = None):
     if backend == "nccl":
         lr = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(lr)
-        dist.init_process_group(backend, device_id=torch.device("cuda", lr))
+        dist.init_process_group(backend, device_id=torch.device("cuda", lr), pg_options=rccl_options())
     else:
         dist.init_process_group(backend)
     return dist.get_rank(), dist.get_world_size()

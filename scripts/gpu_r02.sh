@@ -8,6 +8,11 @@ mkdir -p gpurun_out
 if [ "${TESTS:-1}" = 1 ]; then
   bash scripts/gpu_tests.sh || exit $?
 fi
+if [ -n "${PYTEST_ONLY:-}" ]; then
+  timeout -k 10 600 python -u -m pytest $PYTEST_ONLY -x -v -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider \
+    > gpurun_out/pytest_only.log 2>&1 || { tail -40 gpurun_out/pytest_only.log; exit 1; }
+  tail -3 gpurun_out/pytest_only.log
+fi
 if [ -n "${CONFIGS:-}" ]; then
   CONFIGS="$CONFIGS" TAG=${TAG:-r02a} timeout -k 10 900 bash scripts/profile.sh > gpurun_out/profile.log 2>&1 \
     || { tail -30 gpurun_out/profile.log; exit 1; }
@@ -22,10 +27,13 @@ if [ "${HALO:-0}" = 1 ]; then
   # per-rank cost of the J-strip exchange machinery: the rank is its own periodic neighbour
   # through RCCL; bench lines with and without the halo path, then a kernel trace of the halo run
   export RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533
-  for a in "" "--halo-selfcomm" "--halo-selfcomm --no-overlap"; do
-    timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 $a 2>> gpurun_out/halo.err | tee -a gpurun_out/halo.log || exit 1
+  for m in main side; do
+    GTMI_HALO_STREAM=$m timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 --halo-selfcomm 2>> gpurun_out/halo.err | tee -a gpurun_out/halo.log || exit 1
   done
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/halo_kt -o kt -- python3 bench.py --no-extra --no-cpu-baseline --steps 20 --halo-selfcomm > gpurun_out/halo_kt.log 2>&1 || exit 1
+  timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 --halo-selfcomm --no-overlap 2>> gpurun_out/halo.err | tee -a gpurun_out/halo.log || exit 1
+  for m in main side; do
+    GTMI_HALO_STREAM=$m timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/halo_kt_$m -o kt -- python3 bench.py --no-extra --no-cpu-baseline --steps 20 --halo-selfcomm > gpurun_out/halo_kt_$m.log 2>&1 || exit 1
+  done
   unset RANK LOCAL_RANK WORLD_SIZE MASTER_ADDR MASTER_PORT
 fi
 if [ "${BENCH:-0}" = 1 ]; then

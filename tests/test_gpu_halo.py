@@ -2,8 +2,9 @@
 
 A world-size-1 NCCL (= RCCL) process group is created in-process (TCP store on 127.0.0.1, no
 torchrun). With ``periodic`` + ``force_comm`` the rank is its own neighbour, so every halo
-face goes pack kernel -> RCCL send/recv -> unpack kernel on the halo stream while the interior
-kernel runs on the compute stream -- the same code the N-GPU bench runs
+face goes pack kernel -> RCCL send/recv -> unpack kernel while the interior kernel runs (both
+stream orderings: everything on the caller's stream with RCCL on its own, the default; or a
+dedicated halo stream) -- the same code the N-GPU bench runs
 (``distributed/halo.py`` HaloStencil, ``distributed/decomp2d.py`` HaloStencil2D).
 Halos start as NaN; only a correct exchange fills them. Each of 3 iterations feeds the result
 back as the next input, and must equal the C oracle's hdiff on the wrap-padded input bit for bit.
@@ -37,8 +38,10 @@ def rccl_group():
         pytest.skip("needs a ROCm GPU")
     os.environ.setdefault("NCCL_DEBUG", "WARN")
     torch.cuda.set_device(0)
+    from gt4py_amd.distributed.halo import rccl_options
+
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
+                            device_id=torch.device("cuda", 0), pg_options=rccl_options())
     yield dist
     dist.destroy_process_group()
 
@@ -67,8 +70,9 @@ def _oracle_hdiff(core, coeff, h, wrap_i):
     return out, padded
 
 
+@pytest.mark.parametrize("stream_mode", ["main", "side"])
 @pytest.mark.parametrize("mode", ["jstrips", "tiles2d", "tiles2d_jperiodic"])
-def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode):
+def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     import torch
 
     from gt4py_amd import storage
@@ -89,6 +93,7 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode):
     else:
         dec = Decomposition2D(ni, nj, 1, 1, (wrap_i, True))
         run = HaloStencil2D(st, ["in_field"], dec, 0, (h, h), force_comm=True)
+    run.stream_mode = stream_mode
     assert run.overlap, "the interior/exchange overlap path must be the one under test"
     for it in range(3):
         ref, padded = _oracle_hdiff(core, coeff_h, h, wrap_i)
@@ -101,6 +106,6 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode):
         fin = storage.from_array(start, backend="gt:mi355x", aligned_index=(h, h, 0))
         run({"in_field": fin, "out_field": out, "coeff": coeff}, origin, (ni, nj, nk))
         torch.cuda.synchronize()
-        gu.assert_match(storage.to_numpy(out), ref, name=f"halo_{mode}_it{it}")
+        gu.assert_match(storage.to_numpy(out), ref, name=f"halo_{mode}_{stream_mode}_it{it}")
         np.testing.assert_array_equal(storage.to_numpy(fin), padded)  # halos hold the neighbours' rows
         core = ref
