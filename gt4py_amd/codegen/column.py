@@ -36,6 +36,7 @@ from gt4py_amd.codegen.common import (  # noqa: F401
 
 LDS_BYTES = 160 * 1024  # per CU (MI355X_MICROARCH.md); one 256-thread block may take all of it
 DEFAULT_RING = 8
+DEFAULT_KREG = 0  # register band levels (option ``kreg``)
 
 
 @dataclasses.dataclass
@@ -81,7 +82,9 @@ class ColumnGen:
                     ilo, ihi, jlo, jhi = max(ilo, a), max(ihi, b), max(jlo, c), max(jhi, d)
         self.ext = (ilo, ihi, jlo, jhi)
         self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
+        self.seg_tail = int(opts.get("seg_tail", 0)) == 1
         self.info = {li: self._analyse_loop(li) for li in kernel.loops}
+        self.kreg = 0
         self.tail = self._plan_tail()
 
     def _mem(self, name):
@@ -190,7 +193,43 @@ class ColumnGen:
         if self.tail_lmax < 1:
             return None
         self.tail_per_level = per_level
+        self._plan_register_band(best)
         return best
+
+    def _plan_register_band(self, t: _Tail) -> None:
+        """Register band: the ``kreg`` levels at the END of loop ``a``'s sweep (the START of loop
+        ``b``'s) keep the tail fields in registers ``rb_<name>_<u>`` instead of LDS; the LDS band
+        moves next to it. The band code is unrolled with static register names, so every band
+        level's section must be known statically: true for ``nk >= band_nmin`` (checked at run time;
+        below it the kernel runs without the register band)."""
+        self.kreg = 0
+        R = int(self.opts.get("kreg", DEFAULT_KREG))
+        if R <= 0:
+            return
+        B = self.info[t.b]
+        if any(B.win.get((n, 0, 0)) != [0, 0] for n in t.fields):
+            return  # the reader's fronts must be the cached level itself
+        maps = {}
+        bounds = []
+        for li in (t.a, t.b):
+            secs = self.st.vertical_loops[li].sections
+            m = []
+            for u in range(R):
+                lev = (ir.LevelMarker.END, u - R) if t.a_fwd else (ir.LevelMarker.START, u)
+                hit = [si for si, sec in enumerate(secs)
+                       if _ge(lev, sec.interval.start) and not _ge(lev, sec.interval.end)]
+                m.append(hit[0] if hit else None)
+            if li == t.a and any(x is None for x in m):
+                return
+            maps[li] = m
+            for sec in secs:
+                bounds += [sec.interval.start, sec.interval.end]
+        nmin = R + 1
+        for b in bounds:
+            nmin = max(nmin, R + (b.offset if b.level == ir.LevelMarker.START else -b.offset) + 1)
+        self.kreg = R
+        self.band_map = maps
+        self.band_nmin = nmin
 
     def _touching_loops(self, name) -> Set[int]:
         out = set()
@@ -283,10 +322,20 @@ class ColumnGen:
             t = self.tail
             B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
             B.append(f"const int tid = (int)(threadIdx.y * {bx} + threadIdx.x);")
-            if t.a_fwd:
-                B.append("const int tc0 = nk - p.tail_len, tc1 = nk;  // cached levels [tc0, tc1)")
+            if self.kreg:
+                R = self.kreg
+                B.append(f"const bool regband = nk >= {self.band_nmin};  // register band of {R} levels")
+                B.append(f"const int rbase = regband ? {R} : 0;")
+                for n in t.fields:
+                    ct = self.st.decl(n).dtype.ctype
+                    B.append(f"{ct} " + ", ".join(f"rb_{cname(n)}_{u}" for u in range(R)) + ";")
             else:
-                B.append("const int tc0 = 0, tc1 = p.tail_len;  // cached levels [tc0, tc1)")
+                B.append("const int rbase = 0;")
+            B.append("const int tlen = p.tail_len < nk - rbase ? p.tail_len : nk - rbase;")
+            if t.a_fwd:
+                B.append("const int tc1 = nk - rbase, tc0 = tc1 - tlen;  // LDS-cached levels [tc0, tc1)")
+            else:
+                B.append("const int tc0 = rbase, tc1 = rbase + tlen;  // LDS-cached levels [tc0, tc1)")
             off = "0"
             for n in t.fields:
                 ct = self.st.decl(n).dtype.ctype
@@ -349,6 +398,8 @@ class ColumnGen:
         tail_write = tail.fields if (tail is not None and tail.a == li) else []
         tail_read = set(tail.fields) if (tail is not None and tail.b == li) else set()
         no_store = tail.no_store if (tail is not None and tail.a == li) else set()
+        R = self.kreg if (tail is not None and li in (tail.a, tail.b)) else 0
+        band_map = self.band_map[li] if R else None
         decl_dtype = {}
         for (name, di, dj) in win:
             decl_dtype[name] = self.st.decl(name).dtype
@@ -368,9 +419,12 @@ class ColumnGen:
             nt = "true" if (name in self.nt_loads and name not in direct) else "false"
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
 
-        def load_into(var, name, di, dj, kexpr, maybe_cached=True) -> List[str]:
+        def load_into(var, name, di, dj, kexpr, maybe_cached=True, reg=None) -> List[str]:
             """``var = F(level kexpr)``: from the LDS tail cache when this loop reads a cached level
-            (a run-time test unless ``maybe_cached`` is False: the level is known not to be cached)."""
+            (a run-time test unless ``maybe_cached`` is False: the level is known not to be cached);
+            ``reg``: the level's static register-band index (register band levels only)."""
+            if reg is not None and name in tail_read and (di, dj) == (0, 0) and 0 <= reg < R:
+                return [f"{var} = rb_{cname(name)}_{reg};"]
             if maybe_cached and name in tail_read and (di, dj) == (0, 0):
                 return [
                     f"{{ const int lv_ = {kexpr};",
@@ -379,11 +433,19 @@ class ColumnGen:
                 ]
             return [f"{var} = {mem_index(name, di, dj, kexpr)};"]
 
+        reg_now = [None]  # static register-band index of the level being generated
+        band_now = [None]  # tail writer: None = run-time test per level, True/False = levels known in/out of the cache
+
         def mem_store(name, kexpr, value):
             nt = "true" if (name in self.nt_stores and name not in direct) else "false"
             st = f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
             if name in no_store and kexpr == "k":
-                st = f"if (k < tc0 || k >= tc1) {st}"
+                if band_now[0] == "reg":
+                    return "// register band level: kept in registers only"
+                if band_now[0] is True:
+                    return "// cached level: kept in LDS only"
+                if band_now[0] is None:
+                    st = f"if (k < tc0 || k >= tc1) {st}"
             return st
 
         P = self.ring
@@ -433,11 +495,15 @@ class ColumnGen:
         # fronts of tail-cached fields in the reading loop (LDS source in the cached segment)
         tail_keys = [key for key, fl in front_load.items() if fl and key[0] in tail_read and key[1:] == (0, 0)]
 
+        sec_start = len(out)
+        band_code: List[str] = []
         for si, sec in enumerate(vl.sections):
             lo, hi = interval_bounds(sec.interval)
             out.append(f"    {{  // section {si}")
             out.append(f"        int ks = {lo}, ke = {hi};")
             out.append("        if (ks < 0) ks = 0; if (ke > nk) ke = nk;")
+            if R:  # the register band's levels run in the unrolled band code
+                out.append("        if (ke > nk - rbase) ke = nk - rbase;" if tail.a_fwd else "        if (ks < rbase) ks = rbase;")
 
             def kaddr(acc: ir.FieldAccess) -> str:
                 kexpr = f"k + ({acc.offset[2]})"
@@ -454,9 +520,10 @@ class ColumnGen:
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
             self._kaddr = kaddr
 
-            def shift_and_fronts(slot: Optional[int], mode: str) -> List[str]:
+            def shift_and_fronts(slot: Optional[int], mode: str, reg_u: Optional[int] = None) -> List[str]:
                 """Shift every window one level and load each front: from ring ``slot``, from the
-                LDS tail cache (``mode`` "lds"), or from memory here (``slot`` None)."""
+                LDS tail cache (``mode`` "lds"), from the register band (``reg_u``: the level's band
+                index) or from memory here (``slot`` None)."""
                 body = []
                 for key, rng in win.items():
                     name, di, dj = key
@@ -470,7 +537,9 @@ class ColumnGen:
                     if front_load[key]:
                         fd = front[key]
                         fv = wvar(name, di, dj, fd)
-                        if mode == "lds" and key in tail_keys:
+                        if reg_u is not None:
+                            body += load_into(fv, name, di, dj, f"k + ({fd})", maybe_cached=False, reg=reg_u + fd)
+                        elif mode == "lds" and key in tail_keys:
                             body.append(f"{fv} = {tail.var(name)}[(k + ({fd}) - tc0) * 256 + tid];")
                         elif slot is not None and key in ring_keys:
                             body.append(f"{fv} = rg{slot}_{fv};")
@@ -478,7 +547,7 @@ class ColumnGen:
                             body += load_into(fv, name, di, dj, f"k + ({fd})", maybe_cached=(mode == "mixed"))
                 return body
 
-            def reload() -> List[str]:
+            def reload(reg_u: Optional[int] = None) -> List[str]:
                 body = []
                 for (name, di, dj), rng in win.items():
                     if not self._mem(name):
@@ -486,7 +555,8 @@ class ColumnGen:
                     for d in range(rng[0], rng[1] + 1):
                         if d == 0 and not zero_needed_in(name, di, dj, sec):
                             continue
-                        body += load_into(wvar(name, di, dj, d), name, di, dj, f"k + ({d})")
+                        body += load_into(wvar(name, di, dj, d), name, di, dj, f"k + ({d})",
+                                          reg=None if reg_u is None else reg_u + d)
                 return body
 
             def statements() -> List[str]:
@@ -497,11 +567,18 @@ class ColumnGen:
                     if g:
                         code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
                     body += code
-                if tail_write:
-                    body.append("if (k >= tc0 && k < tc1) {  // LDS tail cache: this level's final values")
-                    for n in tail_write:
-                        body.append(f"    {tail.var(n)}[(k - tc0) * 256 + tid] = {wvar(n, 0, 0, 0)};")
-                    body.append("}")
+                if tail_write and band_now[0] == "reg":
+                    body.append("// register band: this level's final values")
+                    body += [f"rb_{cname(n)}_{reg_now[0]} = {wvar(n, 0, 0, 0)};" for n in tail_write]
+                elif tail_write and band_now[0] is not False:
+                    stores = [f"{tail.var(n)}[(k - tc0) * 256 + tid] = {wvar(n, 0, 0, 0)};" for n in tail_write]
+                    if band_now[0] is True:
+                        body.append("// LDS tail cache: this level's final values")
+                        body += stores
+                    else:
+                        body.append("if (k >= tc0 && k < tc1) {  // LDS tail cache: this level's final values")
+                        body += ["    " + x for x in stores]
+                        body.append("}")
                 return body
 
             def entry_level(slot, mode) -> List[str]:
@@ -584,7 +661,18 @@ class ColumnGen:
                 o.append("}")
                 return o
 
-            if tail_keys:
+            if tail_write and self.seg_tail:
+                # tail writer: the levels before the cached band (in sweep order) and the band
+                # itself run as separate segments, so no level tests whether it is cached
+                if fwd:
+                    parts = [("ks", "(ke < tc0 ? ke : tc0)", False), ("(ks > tc0 ? ks : tc0)", "ke", True)]
+                else:
+                    parts = [("(ks > tc1 ? ks : tc1)", "ke", False), ("ks", "(ke < tc1 ? ke : tc1)", True)]
+                for ss, se, band in parts:
+                    band_now[0] = band
+                    out += ["        " + x for x in segment(ss, se, "mem")]
+                band_now[0] = None
+            elif tail_keys:
                 # split the section by where the tail-cached fronts come from. A front k + fd is
                 # cached iff tc0 <= k + fd < tc1. With lo/hi the smallest/largest fd of the tail keys:
                 # all fronts cached for k in [tc0 - lo, tc1 - hi), none below tc0 - hi or from
@@ -610,6 +698,30 @@ class ColumnGen:
             else:
                 out += ["        " + x for x in segment("ks", "ke", "mem")]
             out.append("    }")
+            us = [u for u in range(R) if band_map[u] == si] if R else []
+            if us:
+                # this section's register-band levels: unrolled, static register names
+                bc = [f"    if (regband) {{  // section {si}: register band levels"]
+                for n_, u in enumerate(sorted(us, reverse=not fwd)):
+                    kexpr = f"nk - {R} + {u}" if tail.a_fwd else f"{u}"
+                    reg_now[0], band_now[0] = u, "reg"
+                    if n_ == 0:
+                        body = (["if (k != k_next) {"] + ["    " + x for x in reload(u)] + ["} else {"]
+                                + ["    " + x for x in shift_and_fronts(None, "mem", u)] + ["}"])
+                    else:
+                        body = shift_and_fronts(None, "mem", u)
+                    body += statements()
+                    reg_now[0], band_now[0] = None, None
+                    bc.append(f"        {{  const int k = {kexpr};")
+                    bc += ["            " + x for x in body]
+                    bc.append("        }")
+                bc.append("    }")
+                band_code += bc
+        if band_code:
+            if li == tail.a:
+                out += band_code  # the band ends the writer's sweep
+            else:
+                out[sec_start:sec_start] = band_code  # and starts the reader's
         out.append("}")
         return out
 
@@ -670,6 +782,14 @@ def _covers_all_levels(vl: ir.VerticalLoop, fwd: bool) -> bool:
     lo = first.start if fwd else last.start
     hi = last.end if fwd else first.end
     return _bound_eq(lo, ir.AxisBound(ir.LevelMarker.START, 0)) and _bound_eq(hi, ir.AxisBound(ir.LevelMarker.END, 0))
+
+
+def _ge(level, bound: ir.AxisBound) -> bool:
+    """``level >= bound`` for every ``nk >= band_nmin`` (``level`` = (marker, offset))."""
+    lm, lo = level
+    if lm == bound.level:
+        return lo >= bound.offset
+    return lm == ir.LevelMarker.END  # END + x >= START + c and not START + x >= END + c, for nk large
 
 
 def _section_ring(itv: ir.Interval, P: int) -> int:
