@@ -106,6 +106,7 @@ def generate(
         "kernels": [type(k).__name__ for k in plan.kernels],
     }
     sig_json = json.dumps(signature).replace("\\", "\\\\").replace('"', '\\"')
+    roctx_name = "gtmi:" + "".join(c if (c.isalnum() or c in "._-") else "_" for c in st.name)
     n_scalars = len(st.scalar_params())
     host_scalars = [
         f"    {sp.dtype.ctype} hs_{cname(sp.name)}; memcpy(&hs_{cname(sp.name)}, &sc[{i}], sizeof(hs_{cname(sp.name)})); "
@@ -115,6 +116,7 @@ def generate(
     src = f"""// Generated by gt4py_amd (gt:mi355x). Do not edit.
 #include "gtmi_device.h"
 #include "gtmi.h"
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <string.h>
 #include <stdio.h>
 
@@ -139,8 +141,10 @@ extern "C" int gtmi_stencil_run(const int64_t* domain, const gtmi_field* f, int3
     hipStream_t stream = (hipStream_t)stream_ptr;
     const int ni = (int)domain[0], nj = (int)domain[1], nk = (int)domain[2];
     (void)ni; (void)nj; (void)nk;
+    roctxRangePushA("{roctx_name}");  // ROCTX range around the launches (rocprofv3 --marker-trace)
 {chr(10).join(host_scalars)}
 {chr(10).join("    " + line for h in launches for line in h.splitlines())}
+    roctxRangePop();
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {{
         snprintf(g_gtmi_err, sizeof(g_gtmi_err), "HIP launch failed: %s", hipGetErrorString(err));

@@ -608,7 +608,7 @@ class PlaneGen:
                 )
             H.append("            p.n_chunks = (nj + p.jc - 1) / p.jc;")
             H.append("            const long long nblocks = (long long)p.n_sgroups * p.n_chunks * p.nks;")
-            H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); return 2; }")
+            H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); roctxRangePop(); return 2; }")
             H.append("            p.perm_a = gtmi_coprime_multiplier((long long)nblocks);")
             H.append(
                 f"            hipLaunchKernelGGL({g['kname']}, dim3((unsigned)nblocks), "

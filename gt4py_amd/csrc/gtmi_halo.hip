@@ -8,6 +8,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "gtmi_halo.h"
 
 #define GTMI_HALO_LAUNCH_BOXES 16  // boxes passed by value per launch (kernel-argument budget)
@@ -55,7 +57,16 @@ __global__ void __launch_bounds__(256) gtmi_halo_kernel(const LaunchBoxes boxes,
 extern "C" const char* gtmi_halo_last_error(void) { return g_err; }
 extern "C" int gtmi_halo_abi_version(void) { return GTMI_HALO_ABI_VERSION; }
 
+static int halo_copy_impl(const gtmi_box* boxes, int32_t n_boxes, int32_t direction, void* stream_ptr);
+
 extern "C" int gtmi_halo_copy(const gtmi_box* boxes, int32_t n_boxes, int32_t direction, void* stream_ptr) {
+    roctxRangePushA(direction == 0 ? "gtmi_halo:pack" : "gtmi_halo:unpack");
+    const int rc = halo_copy_impl(boxes, n_boxes, direction, stream_ptr);
+    roctxRangePop();
+    return rc;
+}
+
+static int halo_copy_impl(const gtmi_box* boxes, int32_t n_boxes, int32_t direction, void* stream_ptr) {
     g_err[0] = 0;
     if (n_boxes < 0 || n_boxes > GTMI_HALO_MAX_BOXES || (direction != 0 && direction != 1)) {
         snprintf(g_err, sizeof(g_err), "bad arguments: n_boxes=%d direction=%d", (int)n_boxes, (int)direction);

@@ -37,6 +37,10 @@ BASE_FLAGS = [
     "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wno-unused-variable",
     "-Wno-unused-but-set-variable",
+    # ROCTX ranges around every stencil call (rocprofv3 --marker-trace shows them by stencil name)
+    "-L/opt/rocm/lib",
+    "-lrocprofiler-sdk-roctx",
+    "-Wl,-rpath,/opt/rocm/lib",
 ]
 
 

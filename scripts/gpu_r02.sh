@@ -36,6 +36,11 @@ if [ "${HALO:-0}" = 1 ]; then
   done
   unset RANK LOCAL_RANK WORLD_SIZE MASTER_ADDR MASTER_PORT
 fi
+if [ "${ROCTX:-0}" = 1 ]; then
+  # ROCTX ranges of the stencil libraries (gtmi:<stencil>) and the halo copies, next to the kernels
+  timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv -d gpurun_out/roctx -o rt -- python3 bench.py --steps 3 --warmup 1 --no-extra --no-cpu-baseline > gpurun_out/roctx.log 2>&1 || { tail -20 gpurun_out/roctx.log; exit 1; }
+  find gpurun_out/roctx -name "*marker*"
+fi
 if [ "${BENCH:-0}" = 1 ]; then
   timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
   cat gpurun_out/bench.json
