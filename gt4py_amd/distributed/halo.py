@@ -208,6 +208,7 @@ class HaloStencil:
                         and halo_fields_read_only(stencil, self.halo_fields))
         self._stream = None
         self.stream_mode = os.environ.get("GTMI_HALO_STREAM", "side")
+        self.split = max(1, int(os.environ.get("GTMI_HALO_SPLIT", "1")))
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
@@ -242,8 +243,13 @@ class HaloStencil:
             self._stream.wait_event(ready)
             with torch.cuda.stream(self._stream):
                 works = self.exchange.start(fields)
-            # the transfers are posted before the interior is enqueued
-            self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
+            # the transfers are posted before the interior is enqueued; with split > 1 the interior
+            # runs as that many row bands, so CU slots free up between launches
+            rows = nj - 2 * h
+            cuts = [h + rows * q // self.split for q in range(self.split + 1)]
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                if b > a:
+                    self.stencil(**kw, origin=self._shifted(origin, a), domain=(ni, b - a, nk), validate_args=False)
             with torch.cuda.stream(self._stream):
                 self.exchange.finish(works)
             main.wait_stream(self._stream)
