@@ -209,6 +209,7 @@ class HaloStencil:
         self._stream = None
         self.stream_mode = os.environ.get("GTMI_HALO_STREAM", "side")
         self.split = max(1, int(os.environ.get("GTMI_HALO_SPLIT", "1")))
+        self.bands_on_halo = os.environ.get("GTMI_HALO_BANDS", "halo") == "halo"
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
@@ -252,7 +253,13 @@ class HaloStencil:
                     self.stencil(**kw, origin=self._shifted(origin, a), domain=(ni, b - a, nk), validate_args=False)
             with torch.cuda.stream(self._stream):
                 self.exchange.finish(works)
+                if self.bands_on_halo:
+                    # the two boundary strips follow the unpack on the halo stream: no stream
+                    # hand-off between the unpack and them (they write rows the interior does not)
+                    self._strips(kw, origin, ni, nj, nk)
             main.wait_stream(self._stream)
+            if self.bands_on_halo:
+                return
         else:
             # "main" (and the CPU/gloo path): pack on the caller's stream, post the transfers
             # (RCCL's stream waits on the pack), enqueue the interior (rows [h, nj - h): reads rows
@@ -260,6 +267,10 @@ class HaloStencil:
             works = self.exchange.start(fields)
             self.stencil(**kw, origin=self._shifted(origin, h), domain=(ni, nj - 2 * h, nk), validate_args=False)
             self.exchange.finish(works)
+        self._strips(kw, origin, ni, nj, nk)
+
+    def _strips(self, kw, origin, ni, nj, nk):
+        h = self.h
         self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
         self.stencil(**kw, origin=self._shifted(origin, nj - h), domain=(ni, h, nk), validate_args=False)
 
