@@ -33,11 +33,11 @@ def _origin_of(case, name, ndim):
     return tuple(o)[:ndim]
 
 
-def run_case_on_gpu(case):
+def run_case_on_gpu(case, opts=None):
     from gt4py_amd import gtscript, storage
 
     stencil = gtscript.stencil(backend=BACKEND, definition=case.definition, externals=case.externals,
-                               name=f"gpu.{case.name}")
+                               name=f"gpu.{case.name}", **(opts or {}))
     host = case.make_inputs()
     dev = {}
     for k, v in host.items():
@@ -77,6 +77,25 @@ def test_golden_case(name):
     res = run_case_on_gpu(case)
     for k, v in outputs.items():
         gu.assert_match(res[k], v, rtol=case.rtol, atol=case.atol, name=f"{name}:{k}")
+
+
+# column-kernel schedule options (off by default): register band of the tail cache,
+# split cached/uncached writer segments, no tail cache at all, a shallow load ring
+COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tail_bwd_fwd", "tail_bwd_fwd_short",
+                    "tail_fwd_bwd_offsets", "tridiag", "tridiag_k161", "tridiag_k2", "tridiag_k70",
+                    "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80"]
+COLUMN_OPTS = [{"kreg": 32}, {"kreg": 16, "seg_tail": 1}, {"seg_tail": 1}, {"ktail_lds": 0}, {"kring": 3}]
+
+
+@pytest.mark.parametrize("opts", COLUMN_OPTS, ids=lambda o: "_".join(f"{k}{v}" for k, v in o.items()))
+@pytest.mark.parametrize("name", COLUMN_OPT_CASES)
+def test_golden_column_options(name, opts):
+    _torch()
+    case = sc.CASES[name]
+    _, outputs, _ = gu.load(name)
+    res = run_case_on_gpu(case, opts)
+    for k, v in outputs.items():
+        gu.assert_match(res[k], v, rtol=case.rtol, atol=case.atol, name=f"{name}{opts}:{k}")
 
 
 # ---------------------------------------------------------------------------------------
