@@ -276,7 +276,8 @@ class HaloStencil2D:
     """
 
     def __init__(self, stencil, halo_fields: Sequence[str], decomp: Decomposition2D, rank: int,
-                 halo: Tuple[int, int], group=None, overlap: bool = True, force_comm: bool = False):
+                 halo: Tuple[int, int], group=None, overlap: bool = True, force_comm: bool = False,
+                 stream_mode: Optional[str] = None):
         self.stencil = stencil
         self.halo_fields = list(halo_fields)
         self.ex = HaloExchange2D(decomp, rank, halo, group, force_comm=force_comm)
@@ -287,7 +288,9 @@ class HaloStencil2D:
             and halo_fields_read_only(stencil, self.halo_fields)
         )
         self._stream = None
-        self.stream_mode = os.environ.get("GTMI_HALO_STREAM", "side")
+        self.stream_mode = stream_mode or os.environ.get("GTMI_HALO_STREAM", "side")
+        if self.stream_mode not in ("side", "main"):
+            raise ValueError(f"stream_mode must be 'side' or 'main', got {self.stream_mode!r}")
 
     def _run(self, kw, origin, i0, j0, ni, nj, nk):
         if ni <= 0 or nj <= 0:

@@ -196,7 +196,13 @@ class HaloStencil:
     """
 
     def __init__(self, stencil, halo_fields: Sequence[str], nj_local: int, halo: int, rank: int, world_size: int,
-                 group=None, overlap: bool = True, periodic: bool = False, force_comm: bool = False):
+                 group=None, overlap: bool = True, periodic: bool = False, force_comm: bool = False,
+                 stream_mode: Optional[str] = None, split: Optional[int] = None, bands_on_halo: Optional[bool] = None):
+        """GPU scheduling knobs (defaults from ``GTMI_HALO_STREAM`` / ``GTMI_HALO_SPLIT`` /
+        ``GTMI_HALO_BANDS``; measurements in DESIGN.md §6): ``stream_mode`` "side" (exchange on a
+        high-priority halo stream, default) or "main" (pack/unpack on the caller's stream);
+        ``split``: interior launched as that many row bands; ``bands_on_halo``: the boundary
+        strips follow the unpack on the halo stream (default) instead of the caller's stream."""
         self.stencil = stencil
         self.halo_fields = list(halo_fields)
         self.exchange = JHaloExchange(nj_local, halo, rank, world_size, group, periodic, force_comm)
@@ -207,9 +213,12 @@ class HaloStencil:
         self.overlap = (overlap and (world_size > 1 or force_comm) and nj_local > 2 * halo
                         and halo_fields_read_only(stencil, self.halo_fields))
         self._stream = None
-        self.stream_mode = os.environ.get("GTMI_HALO_STREAM", "side")
-        self.split = max(1, int(os.environ.get("GTMI_HALO_SPLIT", "1")))
-        self.bands_on_halo = os.environ.get("GTMI_HALO_BANDS", "halo") == "halo"
+        self.stream_mode = stream_mode or os.environ.get("GTMI_HALO_STREAM", "side")
+        if self.stream_mode not in ("side", "main"):
+            raise ValueError(f"stream_mode must be 'side' or 'main', got {self.stream_mode!r}")
+        self.split = max(1, int(split if split is not None else os.environ.get("GTMI_HALO_SPLIT", "1")))
+        self.bands_on_halo = (bands_on_halo if bands_on_halo is not None
+                              else os.environ.get("GTMI_HALO_BANDS", "halo") == "halo")
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
