@@ -311,7 +311,16 @@ class Workload:
 
         def uniform(shape, lo, hi, aligned=(0, 0, 0)):
             t = alloc(shape, aligned)
-            t.copy_(torch.rand(shape, generator=gen, device=dev, dtype=tdt) * (hi - lo) + lo)
+            if getattr(args, "fill", "bulk") == "bulk":
+                t.copy_(torch.rand(shape, generator=gen, device=dev, dtype=tdt) * (hi - lo) + lo)
+                return t
+            # filled one K slab at a time: no field-sized temporaries, so the caching allocator
+            # holds only the fields themselves (their HBM placement does not depend on freed
+            # temporaries)
+            for k0 in range(0, shape[2], 16):
+                k1 = min(shape[2], k0 + 16)
+                sub = (shape[0], shape[1], k1 - k0)
+                t[:, :, k0:k1].copy_(torch.rand(sub, generator=gen, device=dev, dtype=tdt) * (hi - lo) + lo)
             return t
 
         def zeros(shape):
@@ -490,6 +499,8 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="N=1: skip the extra_configs timings")
     ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--jchunk", type=int, default=None)
+    ap.add_argument("--fill", default="bulk", choices=["slab", "bulk"],
+                    help="synthetic fields filled with field-sized temporaries (default) or per K slab")
     ap.add_argument("--decomp", default="jstrips", choices=["jstrips", "2d"],
                     help="N>1: J strips (default) or a balanced 2-D process grid (corners exchanged)")
     ap.add_argument("--no-overlap", action="store_true",
