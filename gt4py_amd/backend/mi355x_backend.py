@@ -87,6 +87,7 @@ class Mi355xBackend(BaseBackend):
         "kring": {"versioning": True, "type": int, "description": "column kernels: window-front loads in flight (levels)"},
         "ktail_lds": {"versioning": True, "type": int, "description": "column kernels: LDS bytes for the sweep-to-sweep tail cache (0 = off)"},
         "ktail_all": {"versioning": True, "type": int, "description": "column kernels: tail-cache every eligible field (1) or only write-free scratch when there is any (0)"},
+        "dpp": {"versioning": True, "type": int, "description": "plane kernels: +-1-lane I shuffles as DPP wave rotates (1, default) instead of ds_bpermute (0)"},
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "seg_tail": {"versioning": True, "type": int, "description": "column kernels: run the tail writer's cached and uncached levels as separate segments (1)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},

@@ -640,7 +640,10 @@ class PlaneGen:
                 if key not in shuffles:
                     nm = f"sh{len(shuffles)}"
                     shuffles[key] = nm
-                    out.append(f"const {ref.val.dtype.ctype} {nm} = gtmi::shfl({ref.val.c}_{slot}_{r}, {qd});")
+                    if int(self.opts.get("dpp", 1)):  # DPP wave rotate for +-1 lanes (gtmi_device.h)
+                        out.append(f"const {ref.val.dtype.ctype} {nm} = gtmi::shfl_c<{qd}>({ref.val.c}_{slot}_{r});")
+                    else:
+                        out.append(f"const {ref.val.dtype.ctype} {nm} = gtmi::shfl({ref.val.c}_{slot}_{r}, {qd});")
 
         for e in range(V):
 

@@ -41,6 +41,39 @@ GTMI_DEV int16_t shfl(int16_t v, int delta) { return (int16_t)shfl((int32_t)v, d
 GTMI_DEV int8_t shfl(int8_t v, int delta) { return (int8_t)shfl((int32_t)v, delta); }
 GTMI_DEV bool shfl(bool v, int delta) { return shfl((int32_t)v, delta) != 0; }
 
+// Compile-time delta: |delta| == 1 is a DPP wave rotate (v_mov_b32_dpp wave_rol:1 / wave_ror:1,
+// a VALU move with no LDS-crossbar round trip); other deltas fall back to ds_bpermute. Same
+// result as shfl(v, delta): lane l receives the value of lane (l + delta) mod 64.
+template <int D> GTMI_DEV int32_t dpp_rot32(int32_t v) {
+    static_assert(D == 1 || D == -1, "DPP wave rotate by one lane only");
+    return __builtin_amdgcn_update_dpp(0, v, D == 1 ? 0x134 : 0x13C, 0xf, 0xf, false);
+}
+template <int D, typename T> GTMI_DEV T shfl_c(T v) {
+    if constexpr (D == 1 || D == -1) {
+        if constexpr (sizeof(T) == 8) {
+            int64_t x;
+            __builtin_memcpy(&x, &v, 8);
+            const int32_t lo = dpp_rot32<D>((int32_t)(x & 0xffffffff));
+            const int32_t hi = dpp_rot32<D>((int32_t)(x >> 32));
+            const int64_t y = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+            T r;
+            __builtin_memcpy(&r, &y, 8);
+            return r;
+        } else if constexpr (sizeof(T) == 4) {
+            int32_t x;
+            __builtin_memcpy(&x, &v, 4);
+            const int32_t y = dpp_rot32<D>(x);
+            T r;
+            __builtin_memcpy(&r, &y, 4);
+            return r;
+        } else {
+            return shfl(v, D);
+        }
+    } else {
+        return shfl(v, D);
+    }
+}
+
 // ---------------------------------------------------------------- clamps
 GTMI_DEV int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
