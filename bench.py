@@ -298,6 +298,10 @@ class Workload:
         opts = {} if dry_run else {"device_sync": False}
         if args.jchunk and not dry_run:
             opts["jchunk"] = args.jchunk
+        if not dry_run:
+            for kv in args.opt or []:  # codegen options (A/B in separate processes: identical placement)
+                k, v = kv.split("=", 1)
+                opts[k] = int(v) if v.lstrip("-").isdigit() else v
         self.stencil = gtscript.stencil(backend=backend, definition=stencil_defs()[(sname, dtype)],
                                         name=f"bench.{cfg}", externals=EXTERNALS.get(sname, {}), **opts)
         tdt = storage.torch_dtype(dtype)
@@ -499,6 +503,8 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="N=1: skip the extra_configs timings")
     ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--jchunk", type=int, default=None)
+    ap.add_argument("--opt", action="append", default=None, metavar="KEY=VALUE",
+                    help="gt:mi355x codegen option for the headline config (repeatable)")
     ap.add_argument("--fill", default="bulk", choices=["slab", "bulk"],
                     help="synthetic fields filled with field-sized temporaries (default) or per K slab")
     ap.add_argument("--decomp", default="jstrips", choices=["jstrips", "2d"],

@@ -360,6 +360,14 @@ class PlaneGen:
         B.append("const int nb = (int)gridDim.x, b = (int)blockIdx.x;")
         if order == 3:
             B.append("const int w = b;  // natural dispatch order")
+        elif order == 5:
+            # level-synchronous XCD-aware order: every level's work items are cut into 8 contiguous
+            # ranges, one per XCD (blocks are dispatched round-robin over the XCDs), so all XCDs
+            # stream the same few levels at a time while each keeps its neighbours in its own L2
+            B.append("const int per_lvl = p.n_sgroups * p.n_chunks, m8 = (per_lvl + 7) >> 3;")
+            B.append("const int lvl = b / (m8 * 8), loc = b - lvl * m8 * 8;")
+            B.append("const int w = (loc & 7) * m8 + (loc >> 3);")
+            B.append("if (w >= per_lvl) return;  // padding block (whole workgroup)")
         else:
             B.append("// XCD-aware block remap: consecutive work items share an XCD (8 XCDs, round-robin dispatch)")
             B.append("const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;")
@@ -368,7 +376,11 @@ class PlaneGen:
                 B.append("const int w = (int)(((long long)w0x * p.perm_a) % nb);  // bijective scatter")
             else:
                 B.append("const int w = w0x;")
-        if order == 4:  # chunks slowest: chunk c+1 starts as chunk c ends on the same XCD (halo rows warm)
+        if order == 5:
+            B.append("const int sg = w % p.n_sgroups;")
+            B.append("const int chunk = w / p.n_sgroups;")
+            B.append("const int kk = p.k0 + lvl;")
+        elif order == 4:  # chunks slowest: chunk c+1 starts as chunk c ends on the same XCD (halo rows warm)
             B.append("const int sg = w % p.n_sgroups;")
             B.append("const int rest = w / p.n_sgroups;")
             B.append("const int kk = p.k0 + rest % p.nks;")
@@ -607,7 +619,10 @@ class PlaneGen:
                     f"p.nks < {PLANE_TARGET_BLOCKS}LL) p.jc >>= 1;"
                 )
             H.append("            p.n_chunks = (nj + p.jc - 1) / p.jc;")
-            H.append("            const long long nblocks = (long long)p.n_sgroups * p.n_chunks * p.nks;")
+            if int(self.opts.get("order", 0)) == 5:  # per level: padded to a multiple of the 8 XCDs
+                H.append("            const long long nblocks = (long long)(((p.n_sgroups * p.n_chunks + 7) >> 3) * 8) * p.nks;")
+            else:
+                H.append("            const long long nblocks = (long long)p.n_sgroups * p.n_chunks * p.nks;")
             H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); roctxRangePop(); return 2; }")
             H.append("            p.perm_a = gtmi_coprime_multiplier((long long)nblocks);")
             H.append(
