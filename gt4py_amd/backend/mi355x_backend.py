@@ -19,7 +19,7 @@ import time
 
 from gt4py_amd.backend.base import BaseBackend, register
 from gt4py_amd.codegen import hip as hipgen
-from gt4py_amd.codegen.lowering import lower_data_dims, split_phases
+from gt4py_amd.codegen.lowering import fuse_parallel_loops, lower_data_dims, split_phases
 from gt4py_amd.codegen.plan import UnsupportedStencil, make_plan
 from gt4py_amd.runtime import jit
 from gt4py_amd.runtime.launcher import StencilLauncher
@@ -33,6 +33,14 @@ def generate_source(analysis, opts):
     kernel planning, code generation."""
     lowered, components = lower_data_dims(analysis)
     abi = analysis.stencil.field_params()
+    fused = fuse_parallel_loops(lowered) if int(opts.get("fuse", 1)) else lowered
+    if fused is not lowered:
+        try:
+            plan = make_plan(fused, pointwise_plane=bool(opts.get("pointwise_plane", 1)))
+            source, signature = hipgen.generate(fused, plan, opts, abi_fields=abi, components=components)
+            return plan, source, signature
+        except UnsupportedStencil:
+            pass  # the computations as written
     try:
         plan = make_plan(lowered, pointwise_plane=bool(opts.get("pointwise_plane", 1)))
         source, signature = hipgen.generate(lowered, plan, opts, abi_fields=abi, components=components)
@@ -88,6 +96,7 @@ class Mi355xBackend(BaseBackend):
         "ktail_lds": {"versioning": True, "type": int, "description": "column kernels: LDS bytes for the sweep-to-sweep tail cache (0 = off)"},
         "ktail_all": {"versioning": True, "type": int, "description": "column kernels: tail-cache every eligible field (1) or only write-free scratch when there is any (0)"},
         "dpp": {"versioning": True, "type": int, "description": "plane kernels: +-1-lane I shuffles as DPP wave rotates (1, default) instead of ds_bpermute (0)"},
+        "fuse": {"versioning": True, "type": int, "description": "merge adjacent PARALLEL computations over identical intervals into one launch (1, default)"},
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "seg_tail": {"versioning": True, "type": int, "description": "column kernels: run the tail writer's cached and uncached levels as separate segments (1)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},

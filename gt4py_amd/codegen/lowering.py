@@ -227,3 +227,82 @@ def split_phases(analysis: StencilAnalysis) -> StencilAnalysis:
         passes.compute_k_boundary(new),
         analysis.min_k_size,
     )
+
+
+# ------------------------------------------------------------------------------------------
+# fusion of adjacent PARALLEL computations
+# ------------------------------------------------------------------------------------------
+
+
+def _same_intervals(a: ir.VerticalLoop, b: ir.VerticalLoop) -> bool:
+    if len(a.sections) != len(b.sections):
+        return False
+    for sa, sb in zip(a.sections, b.sections):
+        for x, y in ((sa.interval.start, sb.interval.start), (sa.interval.end, sb.interval.end)):
+            if x.level != y.level or x.offset != y.offset:
+                return False
+    return True
+
+
+def _fusable(a: ir.VerticalLoop, b: ir.VerticalLoop, api: set) -> bool:
+    """Can computation ``b`` run inside computation ``a`` (statements appended per section)
+    without changing any result? Both PARALLEL over the same intervals, and the merged loop obeys
+    the parallel model: nothing written by one is read by the other at a K offset (levels of one
+    PARALLEL loop run in any order), no API field written in either is read at an IJ offset in
+    either (the merged loop would read a field it writes across columns), ``a`` reads nothing
+    ``b`` writes, and no run-time K offsets."""
+    if a.loop_order != ir.LoopOrder.PARALLEL or b.loop_order != ir.LoopOrder.PARALLEL:
+        return False
+    if not _same_intervals(a, b):
+        return False
+    acc_a = [x for sec in a.sections for x in passes.iter_accesses(sec.body)]
+    acc_b = [x for sec in b.sections for x in passes.iter_accesses(sec.body)]
+    for acc, _ in acc_a + acc_b:
+        if isinstance(acc, ir.FieldAccess) and acc.k_offset is not None:
+            return False
+    wa = {acc.name for acc, w in acc_a if w}
+    wb = {acc.name for acc, w in acc_b if w}
+    for acc, w in acc_b:
+        if not w and isinstance(acc, ir.FieldAccess) and acc.name in wa and acc.offset[2] != 0:
+            return False
+    for acc, w in acc_a:
+        if not w and acc.name in wb:
+            return False
+    written_api = (wa | wb) & api
+    for acc, w in acc_a + acc_b:
+        if not w and isinstance(acc, ir.FieldAccess) and acc.name in written_api and (acc.offset[0] or acc.offset[1]):
+            return False
+    return True
+
+
+def fuse_parallel_loops(analysis: StencilAnalysis) -> StencilAnalysis:
+    """Merge consecutive PARALLEL computations over identical intervals into one, so that a
+    temporary one computation produces and the next reads at IJ offsets lives in the plane
+    kernel's register rings instead of a scratch field round trip through HBM (e.g. hdiff
+    written as lap / flux / update blocks runs as ONE launch, like the single-block form).
+    The reference keeps such computations as separate vertical loops (its AdjacentLoopMerging,
+    ``gtc/passes/oir_optimizations/vertical_loop_merging.py:16-29``, only joins loops whose
+    intervals touch); merging here changes no result (same statements, same order per point)."""
+    st = analysis.stencil
+    api = {p.name for p in st.field_params()}
+    loops: List[ir.VerticalLoop] = []
+    for vl in st.vertical_loops:
+        if loops and _fusable(loops[-1], vl, api):
+            prev = loops[-1]
+            loops[-1] = ir.VerticalLoop(
+                prev.loop_order,
+                [ir.Section(sa.interval, list(sa.body) + list(sb.body), sa.def_index)
+                 for sa, sb in zip(prev.sections, vl.sections)],
+            )
+        else:
+            loops.append(vl)
+    if len(loops) == len(st.vertical_loops):
+        return analysis
+    new = dataclasses.replace(st, vertical_loops=loops)
+    return StencilAnalysis(
+        new,
+        passes.compute_access_kinds(new),
+        passes.compute_extents(new),
+        passes.compute_k_boundary(new),
+        analysis.min_k_size,
+    )

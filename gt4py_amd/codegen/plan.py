@@ -180,10 +180,27 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_pl
             for acc, w in _loop_accesses(vl):
                 if not w and isinstance(acc, ir.FieldAccess) and acc.name in temps and acc.offset[2] != 0:
                     gap_read.add(acc.name)
+    def section_local(name: str, li: int) -> bool:
+        """Every section of loop ``li`` that touches ``name`` writes it and reads it at its own
+        level only: the plane kernels of the sections never hand a value to each other."""
+        for sec in st.vertical_loops[li].sections:
+            accs = [(a, w) for a, w in iter_accesses(sec.body) if a.name == name]
+            if not accs:
+                continue
+            if not any(w for _, w in accs):
+                return False
+            if any(isinstance(a, ir.FieldAccess) and (a.offset[2] != 0 or a.k_offset is not None) for a, _ in accs):
+                return False
+        return True
+
     scratch = []
     for t in st.temporaries:
         kk = touch_kernels.get(t.name, set())
         ll = touch_loops.get(t.name, set())
+        if len(kk) > 1 and len(ll) == 1 and t.name not in gap_read and all(
+            isinstance(kernels[ki], PlaneKernel) for ki in kk
+        ) and section_local(t.name, next(iter(ll))):
+            continue  # per-section plane kernels of one loop, each producing its own values
         if len(kk) > 1 or len(ll) > 1 or t.name in gap_read:
             scratch.append(t.name)
     # column kernels must not read scratch temporaries written inside the same kernel at IJ offsets
