@@ -44,6 +44,8 @@ CONFIGS = {
     "copy": ("copy_stencil", np.float64, (1024, 1024, 160), 0, 16),
     # the canonical production K-sweep (5 fields read, 1 written)
     "vadv": ("vertical_advection_dycore", np.float64, (1024, 1024, 160), 0, 48),
+    # hdiff written as three computations (lap / fluxes / update): fused into one launch
+    "hdiff_blocks": ("horizontal_diffusion_blocks", np.float64, (2048, 2048, 160), 2, 24),
 }
 
 
@@ -145,7 +147,23 @@ def stencil_defs():
                 datacol = dcol[0, 0, 0] - ccol[0, 0, 0] * datacol[0, 0, 1]
                 utens_stage = dtr_stage * (datacol - u_pos[0, 0, 0])
 
+    def horizontal_diffusion_blocks(in_field: F64, out_field: F64, coeff: F64):
+        with computation(PARALLEL), interval(...):
+            lap = 4.0 * in_field[0, 0, 0] - (
+                in_field[1, 0, 0] + in_field[-1, 0, 0] + in_field[0, 1, 0] + in_field[0, -1, 0]
+            )
+        with computation(PARALLEL), interval(...):
+            res = lap[1, 0, 0] - lap[0, 0, 0]
+            flx = 0 if (res * (in_field[1, 0, 0] - in_field[0, 0, 0])) > 0 else res
+            res_j = lap[0, 1, 0] - lap[0, 0, 0]
+            fly = 0 if (res_j * (in_field[0, 1, 0] - in_field[0, 0, 0])) > 0 else res_j
+        with computation(PARALLEL), interval(...):
+            out_field = in_field[0, 0, 0] - coeff[0, 0, 0] * (
+                flx[0, 0, 0] - flx[-1, 0, 0] + fly[0, 0, 0] - fly[0, -1, 0]
+            )
+
     return {
+        ("horizontal_diffusion_blocks", np.float64): horizontal_diffusion_blocks,
         ("vertical_advection_dycore", np.float64): vertical_advection_dycore,
         ("horizontal_diffusion", np.float64): make_hdiff(np.float64),
         ("horizontal_diffusion", np.float32): make_hdiff(np.float32),
@@ -335,12 +353,12 @@ class Workload:
         self.halo = None
         self.named = None
         self.params = {}
-        if sname in ("horizontal_diffusion", "lap5"):
+        if sname in ("horizontal_diffusion", "horizontal_diffusion_blocks", "lap5"):
             fin = uniform((ni + 2 * h, nj + 2 * h, nk), -10, 10, (h, h, 0))
             out = zeros((ni, nj, nk))
             self.named = {"in_field": fin, "out_field": out}
             self.origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
-            if sname == "horizontal_diffusion":
+            if sname != "lap5":
                 self.named["coeff"] = uniform((ni, nj, nk), 0.0, 0.5)
                 self.origin["coeff"] = (0, 0, 0)
             self.args = tuple(self.named.values())
@@ -438,7 +456,7 @@ def traffic_for(cfg, key):
     return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_{cfg}.json (library {key})"
 
 
-EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv")
+EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv", "hdiff_blocks")
 
 
 # ------------------------------------------------------------------------------------------
