@@ -81,9 +81,7 @@ class StencilLauncher:
     def _scratch_buffers(self, domain, device):
         key = (tuple(domain), str(device))
         if key not in self._scratch_cache:
-            import torch
-
-            from gt4py_amd.storage import torch_dtype
+            from gt4py_amd.storage import staggered_device_buffer
 
             ni, nj, nk = domain
             out = []
@@ -92,10 +90,10 @@ class StencilLauncher:
                 si, sj = ni + ilo + ihi, nj + jlo + jhi
                 pi = -(-si // 32) * 32
                 if "K" in s.get("axes", ("I", "J", "K")):
-                    buf = torch.empty(pi * sj * nk, dtype=torch_dtype(np.dtype(s["dtype"])), device=device)
+                    buf = staggered_device_buffer(pi * sj * nk, np.dtype(s["dtype"]), device)
                     out.append((buf, (si, sj, nk), (1, pi, pi * sj), (ilo, jlo, 0), s["dtype"]))
                 else:  # IJ temporary: one plane shared by every level (K stride 0)
-                    buf = torch.empty(pi * sj, dtype=torch_dtype(np.dtype(s["dtype"])), device=device)
+                    buf = staggered_device_buffer(pi * sj, np.dtype(s["dtype"]), device)
                     out.append((buf, (si, sj, 1), (1, pi, 0), (ilo, jlo, 0), s["dtype"]))
             self._scratch_cache[key] = out
         return self._scratch_cache[key]

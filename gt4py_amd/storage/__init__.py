@@ -13,6 +13,7 @@ from_array``), ``layout_registry.py:13-122`` (per-backend ``LayoutInfo``),
 from __future__ import annotations
 
 import math
+import os
 import numbers
 from typing import Any, Callable, Dict, Optional, Sequence, Tuple
 
@@ -125,9 +126,46 @@ def allocate_cpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
     return raw, arr
 
 
+# HBM placement of large fields: hipMalloc hands out 2 MiB-aligned blocks, so every
+# large field starts at the same address residue modulo 2 MiB, and the K sweeps of the column
+# kernels, which stream all their fields level by level, then collide on the same HBM channels
+# (measured: tridiag 1.97 ms with equal residues, 1.86-1.89 ms when consecutive fields alternate
+# bit 20 of the address; the plane kernels are insensitive). Large allocations therefore place
+# their aligned element at (n mod 2) MiB modulo 2 MiB, n counting large allocations.
+HBM_STAGGER_MIN_BYTES = 64 << 20
+HBM_STAGGER_QUANTUM = 1 << 20
+_stagger_count = 0
+
+
+def hbm_stagger_residue(nbytes: int) -> Optional[int]:
+    """Target address residue (modulo 2 quanta) of the next large device allocation, or None for
+    small ones (and when ``GTMI_HBM_STAGGER=0``)."""
+    global _stagger_count
+    if nbytes < HBM_STAGGER_MIN_BYTES or os.environ.get("GTMI_HBM_STAGGER", "1") == "0":
+        return None
+    r = (_stagger_count % 2) * HBM_STAGGER_QUANTUM
+    _stagger_count += 1
+    return r
+
+
+def staggered_device_buffer(n_elements: int, dtype, device):
+    """A flat device tensor of ``n_elements`` whose first element follows the HBM stagger policy
+    (scratch fields of the generated kernels)."""
+    import torch
+
+    dtype = np.dtype(dtype)
+    residue = hbm_stagger_residue(n_elements * dtype.itemsize)
+    if residue is None:
+        return torch.empty(n_elements, dtype=torch_dtype(dtype), device=device)
+    buf = torch.empty(n_elements + (2 * HBM_STAGGER_QUANTUM) // dtype.itemsize, dtype=torch_dtype(dtype), device=device)
+    off = ((residue - buf.data_ptr()) % (2 * HBM_STAGGER_QUANTUM)) // dtype.itemsize
+    return buf[off:off + n_elements]
+
+
 def allocate_gpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
     """``(flat device buffer, strided tensor view)`` on the current ROCm device, same layout rules
-    as :func:`allocate_cpu` (the reference's CuPy ``allocate_gpu``, ``utils.py:251-316``)."""
+    as :func:`allocate_cpu` (the reference's CuPy ``allocate_gpu``, ``utils.py:251-316``); large
+    fields are staggered in HBM (``hbm_stagger_residue``)."""
     import torch
 
     from gt4py_amd.runtime import device as dev
@@ -138,8 +176,16 @@ def allocate_gpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
     strides, shift, total, align_el = _allocation_plan(
         shape, layout_map, dtype.itemsize, alignment_bytes, aligned_index
     )
-    buf = torch.empty(int(total + align_el), dtype=torch_dtype(dtype), device=dev.current_device())
-    base = ((-buf.data_ptr()) % alignment_bytes) // dtype.itemsize
+    residue = hbm_stagger_residue(total * dtype.itemsize)
+    extra = align_el if residue is None else (2 * HBM_STAGGER_QUANTUM) // dtype.itemsize + align_el
+    buf = torch.empty(int(total + extra), dtype=torch_dtype(dtype), device=dev.current_device())
+    if residue is None:
+        base = ((-buf.data_ptr()) % alignment_bytes) // dtype.itemsize
+    else:
+        # the aligned element lands on an address == residue (mod 2 quanta); the quantum is a
+        # multiple of the alignment, so it stays aligned
+        target = (residue - (buf.data_ptr() + shift * dtype.itemsize)) % (2 * HBM_STAGGER_QUANTUM)
+        base = target // dtype.itemsize
     arr = torch.as_strided(buf, size=shape, stride=strides, storage_offset=int(base + shift))
     return buf, arr
 

@@ -66,10 +66,13 @@ __global__ void __launch_bounds__(256) k_r4w3(const d2* a, const d2* b, d2* c, d
 
 int main(int argc, char** argv) {
     const long long n = (argc > 1 ? atoll(argv[1]) : 2048LL * 2048 * 160) / 2;  // d2 elements per array
+    const int mode = argc > 2 ? atoi(argv[2]) : 0;  // 1: relative-offset sweep (HBM channel aliasing)
     const int reps = 20;
     const size_t B = n * sizeof(d2);
     d2* f[5];
     for (int i = 0; i < 5; ++i) {
+        f[i] = nullptr;
+        if (mode == 1) continue;
         CK(hipMalloc(&f[i], B));
         CK(hipMemset(f[i], 0x3f, B));
     }
@@ -94,9 +97,30 @@ int main(int argc, char** argv) {
         }
         std::sort(ms.begin(), ms.end());
         const double med = ms[ms.size() / 2];
-        printf("%-14s median %.4f ms  %.1f GB/s  frac %.3f\n", name, med, bytes / (med * 1e-3) / 1e9, bytes / (med * 1e-3) / 8e12);
+        printf("%-22s median %.4f ms  %.1f GB/s  frac %.3f\n", name, med, bytes / (med * 1e-3) / 1e9, bytes / (med * 1e-3) / 8e12);
         fflush(stdout);
     };
+    if (mode == 1) {
+        // arrays carved from one arena at base + q * (B + d): the relative offset of the streams
+        // modulo the HBM interleave decides whether they collide on the same channels
+        const size_t maxd = 8ull << 20;
+        char* arena;
+        CK(hipMalloc(&arena, 3 * (B + maxd) + (4 << 20)));
+        CK(hipMemset(arena, 0x3f, 3 * (B + maxd)));
+        const int grid = ncu * 8;
+        for (long long d : {0LL, 4096LL, 65536LL, 262144LL, 524288LL, 786432LL, 1LL << 20, 1536LL << 10, 2LL << 20,
+                            3LL << 20, 4LL << 20, 5LL << 20, 6LL << 20, 7LL << 20}) {
+            d2* a = (d2*)(arena);
+            d2* b = (d2*)(arena + (B + d));
+            d2* c = (d2*)(arena + 2 * (B + d));
+            char label[64];
+            snprintf(label, sizeof label, "copy d=%lld", d);
+            timeit(label, 2.0 * B, [&] { hipLaunchKernelGGL(k_copy<true>, dim3(grid), dim3(256), 0, 0, a, b, n); });
+            snprintf(label, sizeof label, "r2w1 d=%lld", d);
+            timeit(label, 3.0 * B, [&] { hipLaunchKernelGGL(k_r2w1<true>, dim3(grid), dim3(256), 0, 0, a, b, c, n); });
+        }
+        return 0;
+    }
     for (int occ : {8, 16, 32}) {
         const int grid = ncu * occ;
         printf("-- grid %d blocks of 256 (%d per CU), %.2f GB per array\n", grid, occ, B / 1e9);
