@@ -219,3 +219,33 @@ def test_from_array_data_dims(backend):
         storage.from_array(host, (np.float64, (3,)), backend=backend)
     assert storage.from_array(np.arange(6).reshape(1, 2, 3), backend=backend).dtype == np.float64
     assert storage.from_array(np.arange(6).reshape(1, 2, 3), None, backend=backend).dtype == np.arange(1).dtype
+
+
+def test_hbm_stagger_policy_cpu():
+    """Large device allocations alternate their 1 MiB residue; small ones are left alone."""
+    from gt4py_amd import storage as gs
+
+    start = gs._stagger_count
+    assert gs.hbm_stagger_residue(1 << 20) is None
+    rs = [gs.hbm_stagger_residue(gs.HBM_STAGGER_MIN_BYTES) for _ in range(4)]
+    assert rs == [((start + q) % 2) * gs.HBM_STAGGER_QUANTUM for q in range(4)]
+
+
+@pytest.mark.gpu
+def test_hbm_stagger_device_addresses():
+    """The aligned elements of consecutive large gt:mi355x storages alternate address bit 20
+     and stay aligned; the data round-trips."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from gt4py_amd import storage as gs
+
+    shape = (1030, 1024, 16)  # > 64 MiB in f64 with the I padding
+    arrs = [gs.empty(shape, np.float64, backend="gt:mi355x", aligned_index=(2, 2, 0)) for _ in range(4)]
+    addrs = [a[2:, 2:, :].data_ptr() for a in arrs]
+    bits = [(p >> 20) & 1 for p in addrs]
+    assert all(p % 256 == 0 for p in addrs)
+    assert all(bits[q] != bits[q + 1] for q in range(3)), [hex(p) for p in addrs]
+    host = np.random.default_rng(0).uniform(size=shape)
+    a = gs.from_array(host, backend="gt:mi355x", aligned_index=(2, 2, 0))
+    assert np.array_equal(gs.to_numpy(a), host)
