@@ -182,9 +182,10 @@ def allocate_gpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
     if residue is None:
         base = ((-buf.data_ptr()) % alignment_bytes) // dtype.itemsize
     else:
-        # the aligned element lands on an address == residue (mod 2 quanta); the quantum is a
-        # multiple of the alignment, so it stays aligned
-        target = (residue - (buf.data_ptr() + shift * dtype.itemsize)) % (2 * HBM_STAGGER_QUANTUM)
+        # the aligned element (flat index shift + ai_off, a multiple of the alignment) lands on an
+        # address == residue (mod 2 quanta); the quantum is a multiple of the alignment
+        ai_off = sum(int(a) * st for a, st in zip(aligned_index, strides))
+        target = (residue - (buf.data_ptr() + (shift + ai_off) * dtype.itemsize)) % (2 * HBM_STAGGER_QUANTUM)
         base = target // dtype.itemsize
     arr = torch.as_strided(buf, size=shape, stride=strides, storage_offset=int(base + shift))
     return buf, arr
