@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--kpad", default="", help="comma list of K-stride paddings in bytes (sweeps them instead of residues)")
+    ap.add_argument("--ipad", default="", help="comma list of extra I-pitch elements (sweeps them instead of residues)")
     args = ap.parse_args()
     import torch
 
@@ -43,27 +44,39 @@ def main():
         names = ["in_field", "out_field", "coeff"]
         origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
         aligned = [(h, h, 0), (0, 0, 0), (0, 0, 0)]
+    elif sname == "lap5":
+        shapes = [(ni + 2 * h, nj + 2 * h, nk), (ni, nj, nk)]
+        names = ["in_field", "out_field"]
+        origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0)}
+        aligned = [(h, h, 0), (0, 0, 0)]
+    elif sname == "copy_stencil":
+        shapes = [(ni, nj, nk)] * 2
+        names = ["field_a", "field_b"]
+        origin = (0, 0, 0)
+        aligned = [(0, 0, 0)] * 2
     else:
         shapes = [(ni, nj, nk)] * 5
         names = ["inf", "diag", "sup", "rhs", "out"]
         origin = (0, 0, 0)
         aligned = [(0, 0, 0)] * 5
     kpads = [int(x) for x in args.kpad.split(",") if x] or [0]
+    ipads = [int(x) for x in args.ipad.split(",") if x] or [0]
     maxpad = max(kpads)
     raws, geo = [], []
     for shp in shapes:
         pi = -(-shp[0] // 32) * 32
         strides = (1, pi, pi * shp[1])
-        nbytes = (pi * shp[1] * isz + maxpad) * shp[2]
+        nbytes = ((pi + max(ipads)) * shp[1] * isz + maxpad) * shp[2]
         raws.append(torch.empty(nbytes + 2 * WINDOW, dtype=torch.uint8, device="cuda"))
         geo.append((shp, strides))
     gen = torch.Generator(device="cuda")
     gen.manual_seed(3)
 
-    def views(residues, kpad=0):
+    def views(residues, kpad=0, ipad=0):
         out = []
         for (shp, strides), raw, al, res in zip(geo, raws, aligned, residues):
-            strides = (strides[0], strides[1], strides[2] + kpad // isz)
+            pitch = strides[1] + ipad
+            strides = (strides[0], pitch, pitch * shp[1] + kpad // isz)
             base = raw.data_ptr()
             lead = (al[0] * strides[0] + al[1] * strides[1]) * isz  # the aligned element's byte offset
             off = (res - (base + lead)) % WINDOW
@@ -78,15 +91,18 @@ def main():
     ]
     if len(shapes) == 5:
         tuples = [t + (t[1] + t[2], 2 * t[2]) for t in tuples]
-    cases = [(t, 0) for t in tuples]
+    tuples = [t[:len(shapes)] for t in tuples]
+    cases = [(t, 0, 0) for t in tuples]
+    odd = tuple((q % 2) * r for q in range(len(shapes)))
     if args.kpad:
         same = tuple(0 for _ in shapes)
-        odd = tuple((q % 2) * r for q in range(len(shapes)))
-        cases = [(res, kp) for kp in kpads for res in (same, odd)]
+        cases = [(res, kp, 0) for kp in kpads for res in (same, odd)]
+    if args.ipad:
+        cases = [(odd, 0, ip) for ip in ipads] + [(odd, 0, ipads[0])]
     tuples = [c[0] for c in cases]
     sets = []
-    for t, kp in cases:
-        v = views(t, kp)
+    for t, kp, ip in cases:
+        v = views(t, kp, ip)
         for x in v:
             x.copy_(torch.rand(x.shape, generator=gen, device="cuda", dtype=x.dtype))
         sets.append(v)
@@ -103,9 +119,9 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / args.reps)
-    for (t, kp), ts in zip(cases, times):
+    for (t, kp, ip), ts in zip(cases, times):
         med = float(np.median(ts))
-        print(json.dumps({"config": args.config, "kpad_bytes": kp, "residues_MiB": [round(x / MIB, 3) for x in t],
+        print(json.dumps({"config": args.config, "kpad_bytes": kp, "ipad": ip, "residues_MiB": [round(x / MIB, 3) for x in t],
                           "median_ms": round(med, 4),
                           "frac": round(ni * nj * nk * bpc / (med * 1e-3) / 8e12, 4)}), flush=True)
 
