@@ -70,7 +70,7 @@ def _oracle_hdiff(core, coeff, h, wrap_i):
     return out, padded
 
 
-@pytest.mark.parametrize("stream_mode", ["main", "side", "side_bands_main"])
+@pytest.mark.parametrize("stream_mode", ["main", "side", "side_bands_main", "side_split3"])
 @pytest.mark.parametrize("mode", ["jstrips", "tiles2d", "tiles2d_jperiodic"])
 def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     import torch
@@ -96,6 +96,7 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     run.stream_mode = stream_mode.split("_")[0]
     if hasattr(run, "bands_on_halo"):
         run.bands_on_halo = not stream_mode.endswith("bands_main")
+        run.split = 3 if stream_mode.endswith("split3") else 1
     assert run.overlap, "the interior/exchange overlap path must be the one under test"
     for it in range(3):
         ref, padded = _oracle_hdiff(core, coeff_h, h, wrap_i)
