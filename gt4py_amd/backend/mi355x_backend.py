@@ -100,7 +100,7 @@ class Mi355xBackend(BaseBackend):
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "seg_tail": {"versioning": True, "type": int, "description": "column kernels: run the tail writer's cached and uncached levels as separate segments (1)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
-        "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd)"},
+        "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},

@@ -289,7 +289,7 @@ class ColumnGen:
         L.append(f"__global__ void __launch_bounds__({bx * by}) k{k}_column(const K{k}Params p) {{")
         B = []
         eilo, eihi, ejlo, ejhi = self.ext
-        if int(self.opts.get("col_order", 0)) == 1:
+        if int(self.opts.get("col_order", 1)) == 1:
             # XCD-aware: consecutive column blocks (along I, then J) run on one XCD (8 XCDs, round-robin dispatch)
             B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
             B.append("const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);")
