@@ -320,10 +320,15 @@ def init_process_group(backend: Optional[str] = None):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
         backend = os.environ.get("GTMI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    import datetime
+
+    # a rank that never arrives fails the job in minutes instead of hanging it (GTMI_DIST_TIMEOUT s)
+    timeout = datetime.timedelta(seconds=float(os.environ.get("GTMI_DIST_TIMEOUT", "300")))
     if backend == "nccl":
         lr = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(lr)
-        dist.init_process_group(backend, device_id=torch.device("cuda", lr), pg_options=rccl_options())
+        dist.init_process_group(backend, device_id=torch.device("cuda", lr), pg_options=rccl_options(),
+                                timeout=timeout)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=timeout)
     return dist.get_rank(), dist.get_world_size()
