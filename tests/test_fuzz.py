@@ -16,6 +16,8 @@ from gt4py_amd.gtscript import BACKWARD, FORWARD, PARALLEL, Field, I, J, computa
 
 """
 SEEDS = list(range(60)) + list(range(1000, 1060))
+# stress runs: GTMI_FUZZ_EXTRA=N adds N more programs (seeds 5000...)
+SEEDS += list(range(5000, 5000 + int(os.environ.get("GTMI_FUZZ_EXTRA", "0"))))
 
 
 def _shape(seed):
