@@ -369,6 +369,11 @@ class Workload:
             elif world > 1:
                 # J strip of the global domain: the in_field halo moves over RCCL while the interior computes
                 self.halo = HaloStencil(self.stencil, ["in_field"], nj, h, rank, world, overlap=overlap)
+            elif args.halo_selfcomm and args.decomp == "2d":
+                # one 1x1 tile, periodic in I and J: both exchange phases go through RCCL to itself
+                dec = Decomposition2D(ni, nj, 1, 1, (True, True))
+                self.halo = HaloStencil2D(self.stencil, ["in_field"], dec, 0, (h, h), overlap=overlap,
+                                          force_comm=True)
             elif args.halo_selfcomm:
                 self.halo = HaloStencil(self.stencil, ["in_field"], nj, h, 0, 1, periodic=True, force_comm=True,
                                         overlap=overlap)
@@ -639,7 +644,7 @@ def main():
             "backend": backend,
             "parallelism": (f"ij-strips{world}" if dec2d is None else f"ij-tiles{dec2d.pi}x{dec2d.pj}")
             if world > 1
-            else ("single+halo-selfcomm" if args.halo_selfcomm else "single"),
+            else (f"single+halo-selfcomm{'-2d' if args.decomp == '2d' else ''}" if args.halo_selfcomm else "single"),
         },
         "roofline": {
             "bound": "hbm",

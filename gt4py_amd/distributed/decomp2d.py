@@ -19,11 +19,14 @@ Periodic boundaries (optional per axis) wrap the neighbour ranks; a periodic axi
 rank copies its own opposite face. Non-periodic global boundaries keep the caller's halo cells
 (plain input, as in the reference).
 
-Overlap (default, ``GTMI_HALO_STREAM=side``): both phases run on a high-priority halo stream
-(its own hardware queue, ``halo.rccl_options``) while the interior, which reads no halo, runs on
-the caller's stream; the four boundary bands follow once the caller's stream waits on the halo
-stream. ``main``: phase 1 is packed on the caller's stream and handed to RCCL, the interior runs
-while the I faces move, then phase 2 and the bands follow on the caller's stream.
+Overlap (default, ``GTMI_HALO_STREAM=side``): the exchange runs on a high-priority halo stream
+(its own hardware queue, ``halo.rccl_options``). Phase 1 (the I faces, small) completes first;
+the interior ``[0, ni) x [hj, nj-hj)`` -- full width, it now reads only filled I halos -- then
+runs on the caller's stream while phase 2 moves the J faces, and the south/north bands follow
+once the caller's stream waits on the halo stream. ``ifirst=False`` instead overlaps both phases
+with an interior that also excludes west/east bands (measured slower: DESIGN.md §6).
+``main``: phase 1 is packed on the caller's stream and handed to RCCL, the interior runs while
+the I faces move, then phase 2 and the bands follow on the caller's stream.
 """
 
 from __future__ import annotations
@@ -255,6 +258,13 @@ class HaloExchange2D:
             self._phase(group, 0)
             self._phase(group, 1)
 
+    def exchange_phase(self, fields: Sequence, phase: int) -> None:
+        """Only phase ``phase`` (0: I faces, 1: J faces incl. corners) of every dtype group."""
+        if not fields:
+            return
+        for group in self._groups(fields):
+            self._phase(group, phase)
+
     def start(self, fields: Sequence):
         """Post phase 0 (I faces) of every dtype group; ``finish`` completes both phases."""
         if not fields:
@@ -277,7 +287,10 @@ class HaloStencil2D:
 
     def __init__(self, stencil, halo_fields: Sequence[str], decomp: Decomposition2D, rank: int,
                  halo: Tuple[int, int], group=None, overlap: bool = True, force_comm: bool = False,
-                 stream_mode: Optional[str] = None):
+                 stream_mode: Optional[str] = None, ifirst: Optional[bool] = None):
+        """``ifirst`` (side mode; default ``GTMI_HALO2D_IFIRST``, on): exchange the I faces
+        before the interior, which then spans the full I width and overlaps only the J-face
+        phase; off: the interior excludes west/east bands that run after both phases."""
         self.stencil = stencil
         self.halo_fields = list(halo_fields)
         self.ex = HaloExchange2D(decomp, rank, halo, group, force_comm=force_comm)
@@ -291,6 +304,7 @@ class HaloStencil2D:
         self.stream_mode = stream_mode or os.environ.get("GTMI_HALO_STREAM", "side")
         if self.stream_mode not in ("side", "main"):
             raise ValueError(f"stream_mode must be 'side' or 'main', got {self.stream_mode!r}")
+        self.ifirst = (os.environ.get("GTMI_HALO2D_IFIRST", "1") != "0") if ifirst is None else bool(ifirst)
 
     def _run(self, kw, origin, i0, j0, ni, nj, nk):
         if ni <= 0 or nj <= 0:
@@ -298,14 +312,26 @@ class HaloStencil2D:
         org = {k: (o[0] + i0, o[1] + j0, *o[2:]) for k, o in origin.items()}
         self.stencil(**kw, origin=org, domain=(ni, nj, nk), validate_args=False)
 
+    def band_width_i(self) -> int:
+        """Width of the west/east bands. The halo width itself would leave bands a few columns
+        wide, and a plane-kernel wave (one I strip of ~112-224 outputs) would then compute a
+        handful of them per row (measured: +28.6 % per step for 2-column bands on hdiff
+        2048^2x160). So the bands take ``BAND_I`` columns (>= the halo), whole strips of the plane
+        kernel, and the interior shrinks by as much; the work is the same, only its split changes."""
+        w = max(self.hi, self.BAND_I)
+        return w if self.ni > 2 * w else self.hi
+
+    BAND_I = 224  # two f64 / one f32 plane-kernel strip of outputs
+
     def bands(self) -> List[Tuple[int, int, int, int]]:
         """(i0, j0, ni, nj) of the boundary bands around the interior (disjoint, covering)."""
-        hi, hj, ni, nj = self.hi, self.hj, self.ni, self.nj
+        hj, ni, nj = self.hj, self.ni, self.nj
+        wi = self.band_width_i()
         return [
             (0, 0, ni, hj),  # south band, full width
             (0, nj - hj, ni, hj),  # north band, full width
-            (0, hj, hi, nj - 2 * hj),  # west band
-            (ni - hi, hj, hi, nj - 2 * hj),  # east band
+            (0, hj, wi, nj - 2 * hj),  # west band
+            (ni - wi, hj, wi, nj - 2 * hj),  # east band
         ]
 
     def __call__(self, args: Dict, origin: Dict[str, Tuple[int, int, int]], domain: Tuple[int, int, int],
@@ -320,6 +346,7 @@ class HaloStencil2D:
             self.stencil(**kw, origin=origin, domain=domain, validate_args=False)
             return
         hi, hj = self.hi, self.hj
+        wi = self.band_width_i()
         on_gpu = fields and getattr(fields[0], "is_cuda", False) and not _backend_name(self.ex.group) == "gloo"
         if on_gpu and self.stream_mode == "side":
             import torch
@@ -328,15 +355,29 @@ class HaloStencil2D:
                 self._stream = torch.cuda.Stream(device=fields[0].device, priority=-1)
             main = torch.cuda.current_stream(fields[0].device)
             self._stream.wait_stream(main)  # the fields' producers
+            if self.ifirst:
+                # the I faces are ~1/(2 nj) of the field: moving them first costs a few tens of us
+                # unhidden, and in exchange the interior runs full-width (no narrow west/east
+                # bands, which a J-streaming plane kernel computes at a fraction of its rate)
+                with torch.cuda.stream(self._stream):
+                    self.ex.exchange_phase(fields, 0)
+                main.wait_stream(self._stream)
+                with torch.cuda.stream(self._stream):
+                    self.ex.exchange_phase(fields, 1)
+                self._run(kw, origin, 0, hj, ni, nj - 2 * hj, nk)
+                main.wait_stream(self._stream)
+                for i0, j0, bi, bj in self.bands()[:2]:  # south and north, full width
+                    self._run(kw, origin, i0, j0, bi, bj, nk)
+                return
             with torch.cuda.stream(self._stream):
                 self.ex.exchange(fields)
-            self._run(kw, origin, hi, hj, ni - 2 * hi, nj - 2 * hj, nk)
+            self._run(kw, origin, wi, hj, ni - 2 * wi, nj - 2 * hj, nk)
             main.wait_stream(self._stream)
         else:
             # default: phase 0 (I faces) is packed and posted on the caller's stream, the interior
             # runs while RCCL moves it; phase 1 (J faces incl. the received I halos) follows
             pending = self.ex.start(fields)
-            self._run(kw, origin, hi, hj, ni - 2 * hi, nj - 2 * hj, nk)
+            self._run(kw, origin, wi, hj, ni - 2 * wi, nj - 2 * hj, nk)
             self.ex.finish(pending)
         for i0, j0, bi, bj in self.bands():
             self._run(kw, origin, i0, j0, bi, bj, nk)

@@ -97,6 +97,8 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     if hasattr(run, "bands_on_halo"):
         run.bands_on_halo = not stream_mode.endswith("bands_main")
         run.split = 3 if stream_mode.endswith("split3") else 1
+    if hasattr(run, "ifirst"):  # 2-D: "side_bands_main" runs the west/east band variant
+        run.ifirst = not stream_mode.endswith("bands_main")
     assert run.overlap, "the interior/exchange overlap path must be the one under test"
     for it in range(3):
         ref, padded = _oracle_hdiff(core, coeff_h, h, wrap_i)
