@@ -19,14 +19,13 @@ Periodic boundaries (optional per axis) wrap the neighbour ranks; a periodic axi
 rank copies its own opposite face. Non-periodic global boundaries keep the caller's halo cells
 (plain input, as in the reference).
 
-Overlap (default, ``GTMI_HALO_STREAM=side``): the exchange runs on a high-priority halo stream
-(its own hardware queue, ``halo.rccl_options``). Phase 1 (the I faces, small) completes first;
-the interior ``[0, ni) x [hj, nj-hj)`` -- full width, it now reads only filled I halos -- then
-runs on the caller's stream while phase 2 moves the J faces, and the south/north bands follow
-once the caller's stream waits on the halo stream. ``ifirst=False`` instead overlaps both phases
-with an interior that also excludes west/east bands (measured slower: DESIGN.md §6).
-``main``: phase 1 is packed on the caller's stream and handed to RCCL, the interior runs while
-the I faces move, then phase 2 and the bands follow on the caller's stream.
+Overlap: phase 1 (the I faces, small) completes first; the interior ``[0, ni) x [hj, nj-hj)``
+-- full width, it reads only filled I halos -- then runs while phase 2 moves the J faces, and
+the south/north bands follow the unpack. Default ``stream_mode="main"`` (``GTMI_HALO2D_STREAM``):
+packs and unpacks on the caller's stream, RCCL on its own high-priority stream; ``"side"`` puts
+the packs/unpacks on a high-priority halo stream (``halo.rccl_options``; three more cross-queue
+hand-offs per step). ``ifirst=False`` instead overlaps both phases with an interior that also
+excludes west/east bands, run after both phases (measured slower: DESIGN.md §6).
 """
 
 from __future__ import annotations
@@ -265,6 +264,14 @@ class HaloExchange2D:
         for group in self._groups(fields):
             self._phase(group, phase)
 
+    def start_phase(self, fields: Sequence, phase: int):
+        """Post phase ``phase`` of every dtype group; ``finish_phase`` completes it."""
+        return [(group, self._phase_start(group, phase)) for group in self._groups(fields)] if fields else []
+
+    def finish_phase(self, pending) -> None:
+        for _group, state in pending:
+            self._phase_finish(state)
+
     def start(self, fields: Sequence):
         """Post phase 0 (I faces) of every dtype group; ``finish`` completes both phases."""
         if not fields:
@@ -288,7 +295,7 @@ class HaloStencil2D:
     def __init__(self, stencil, halo_fields: Sequence[str], decomp: Decomposition2D, rank: int,
                  halo: Tuple[int, int], group=None, overlap: bool = True, force_comm: bool = False,
                  stream_mode: Optional[str] = None, ifirst: Optional[bool] = None):
-        """``ifirst`` (side mode; default ``GTMI_HALO2D_IFIRST``, on): exchange the I faces
+        """``ifirst`` (default ``GTMI_HALO2D_IFIRST``, on): exchange the I faces
         before the interior, which then spans the full I width and overlaps only the J-face
         phase; off: the interior excludes west/east bands that run after both phases."""
         self.stencil = stencil
@@ -301,7 +308,10 @@ class HaloStencil2D:
             and halo_fields_read_only(stencil, self.halo_fields)
         )
         self._stream = None
-        self.stream_mode = stream_mode or os.environ.get("GTMI_HALO_STREAM", "side")
+        # default "main": with the I faces first nothing overlaps phase 1 anyway, and keeping the
+        # packs/unpacks on the caller's stream saves three cross-queue hand-offs per step
+        # (+6.3-6.7 % vs +6.6-7.2 % for "side")
+        self.stream_mode = stream_mode or os.environ.get("GTMI_HALO2D_STREAM", "main")
         if self.stream_mode not in ("side", "main"):
             raise ValueError(f"stream_mode must be 'side' or 'main', got {self.stream_mode!r}")
         self.ifirst = (os.environ.get("GTMI_HALO2D_IFIRST", "1") != "0") if ifirst is None else bool(ifirst)
@@ -373,9 +383,20 @@ class HaloStencil2D:
                 self.ex.exchange(fields)
             self._run(kw, origin, wi, hj, ni - 2 * wi, nj - 2 * hj, nk)
             main.wait_stream(self._stream)
+        elif self.ifirst:
+            # caller's stream (and the CPU/gloo path): phase 0 whole (pack, RCCL, unpack), then
+            # phase 1 posted, the full-width interior enqueued while it moves, unpack and the
+            # south/north bands -- every hand-off is between the caller's and RCCL's streams
+            self.ex.exchange_phase(fields, 0)
+            pending = self.ex.start_phase(fields, 1)
+            self._run(kw, origin, 0, hj, ni, nj - 2 * hj, nk)
+            self.ex.finish_phase(pending)
+            for i0, j0, bi, bj in self.bands()[:2]:
+                self._run(kw, origin, i0, j0, bi, bj, nk)
+            return
         else:
-            # default: phase 0 (I faces) is packed and posted on the caller's stream, the interior
-            # runs while RCCL moves it; phase 1 (J faces incl. the received I halos) follows
+            # phase 0 (I faces) is packed and posted on the caller's stream, the interior runs
+            # while RCCL moves it; phase 1 (J faces incl. the received I halos) follows
             pending = self.ex.start(fields)
             self._run(kw, origin, wi, hj, ni - 2 * wi, nj - 2 * hj, nk)
             self.ex.finish(pending)

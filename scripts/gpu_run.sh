@@ -27,12 +27,12 @@ if [ "${HALO:-0}" = 1 ]; then
   # per-rank cost of the J-strip exchange machinery: the rank is its own periodic neighbour
   # through RCCL; bench lines with and without the halo path, then a kernel trace of the halo run
   export RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533
-  for m in halo main; do
+  for m in halo unpack_main halo unpack_main; do
     GTMI_HALO_BANDS=$m timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 --halo-selfcomm 2>> gpurun_out/halo.err | tee -a gpurun_out/halo.log || exit 1
   done
   timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 --halo-selfcomm --no-overlap 2>> gpurun_out/halo.err | tee -a gpurun_out/halo.log || exit 1
   timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 --halo-selfcomm --decomp 2d 2>> gpurun_out/halo.err | tee -a gpurun_out/halo.log || exit 1
-  for m in halo; do
+  for m in halo unpack_main; do
     GTMI_HALO_BANDS=$m timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/halo_kt_$m -o kt -- python3 bench.py --no-extra --no-cpu-baseline --steps 20 --halo-selfcomm > gpurun_out/halo_kt_$m.log 2>&1 || exit 1
   done
   unset RANK LOCAL_RANK WORLD_SIZE MASTER_ADDR MASTER_PORT

@@ -70,7 +70,7 @@ def _oracle_hdiff(core, coeff, h, wrap_i):
     return out, padded
 
 
-@pytest.mark.parametrize("stream_mode", ["main", "side", "side_bands_main", "side_split3"])
+@pytest.mark.parametrize("stream_mode", ["main", "main_bands", "side", "side_bands_main", "side_unpack_main", "side_split3"])
 @pytest.mark.parametrize("mode", ["jstrips", "tiles2d", "tiles2d_jperiodic"])
 def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     import torch
@@ -97,8 +97,9 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     if hasattr(run, "bands_on_halo"):
         run.bands_on_halo = not stream_mode.endswith("bands_main")
         run.split = 3 if stream_mode.endswith("split3") else 1
-    if hasattr(run, "ifirst"):  # 2-D: "side_bands_main" runs the west/east band variant
-        run.ifirst = not stream_mode.endswith("bands_main")
+        run.unpack_on_main = stream_mode.endswith("unpack_main")
+    if hasattr(run, "ifirst"):  # 2-D: "*bands*" modes run the west/east band variant
+        run.ifirst = not (stream_mode.endswith("bands_main") or stream_mode == "main_bands")
     assert run.overlap, "the interior/exchange overlap path must be the one under test"
     for it in range(3):
         ref, padded = _oracle_hdiff(core, coeff_h, h, wrap_i)
