@@ -67,7 +67,7 @@ class _Compiled:
         self.options = options
         self.launcher = StencilLauncher(lib_path, analysis.stencil.name)
 
-    def __call__(self, domain, origin, exec_info, kwargs):
+    def __call__(self, domain, origin, exec_info, kwargs, rows=None):
         self.launcher(
             domain,
             origin,
@@ -75,6 +75,7 @@ class _Compiled:
             kwargs,
             device_sync=bool(self.options.get("device_sync", True)),
             exec_info=exec_info,
+            rows=rows,
         )
 
 
@@ -129,10 +130,11 @@ class Mi355xBackend(BaseBackend):
     def make_run_impl(self):
         compiled = self.compile()
 
-        def run_impl(domain, origin, exec_info, kwargs):
-            compiled(domain, origin, exec_info, kwargs)
+        def run_impl(domain, origin, exec_info, kwargs, rows=None):
+            compiled(domain, origin, exec_info, kwargs, rows)
 
         run_impl.compiled = compiled
+        run_impl.supports_rows = True  # gtmi_stencil_run_jsplit
         return run_impl
 
     def make_stencil_class(self):

@@ -48,6 +48,18 @@ from gt4py_amd.codegen.plane import PlaneGen
 # ------------------------------------------------------------------------------------------
 
 
+def jsplit_native(analysis: StencilAnalysis, plan: KernelPlan) -> bool:
+    """``gtmi_stencil_run_jsplit`` runs in one launch per kernel: plane kernels only (their J
+    chunks are mapped around the gap), no scratch (a producer's J halo would straddle it), no
+    horizontal regions (their conditions are relative to the call's domain)."""
+    if plan.scratch or not all(isinstance(k, PlaneKernel) for k in plan.kernels):
+        return False
+    st = analysis.stencil
+    return not any(
+        isinstance(n, ir.HorizontalRegion) for vl in st.vertical_loops for sec in vl.sections for n in ir.walk(sec.body)
+    )
+
+
 def generate(
     analysis: StencilAnalysis, plan: KernelPlan, opts: Dict, abi_fields=None, components=None
 ) -> Tuple[str, Dict]:
@@ -86,7 +98,7 @@ def generate(
     for comp in components.values():
         used_scalars |= {n.name for x in comp.index for n in ir.walk(x) if isinstance(n, ir.ScalarAccess)}
     signature = {
-        "abi": 2,
+        "abi": 3,
         "fields": [
             {"name": p.name, "dtype": p.dtype.name.lower(), "axes": list(p.axes), "data_dims": list(p.data_dims)}
             for p in abi_fields
@@ -113,6 +125,23 @@ def generate(
         f"(void)hs_{cname(sp.name)};"
         for i, sp in enumerate(st.scalar_params())
     ]
+    if jsplit_native(analysis, plan):
+        # every kernel is a plane kernel without scratch or regions: one launch per kernel over both row ranges
+        jsplit_body = "    return gtmi_run_rows(domain, (int)j_split, (int)j_skip, f, sc, stream);"
+    else:
+        # two ordinary passes; the second sees every field (and scratch buffer) shifted by the gap
+        jsplit_body = f"""    if (j_split > 0) {{
+        const int64_t da[3] = {{domain[0], j_split, domain[2]}};
+        if (int rc = gtmi_run_rows(da, (int)j_split, 0, f, sc, stream)) return rc;
+    }}
+    if (rows_b == 0) return 0;
+    gtmi_field g[{max(1, n_fields)}];
+    for (int q = 0; q < {n_fields}; ++q) {{
+        g[q] = f[q];
+        if (g[q].strides[1] != 0) g[q].origin[1] += j_split + j_skip;
+    }}
+    const int64_t db[3] = {{domain[0], rows_b, domain[2]}};
+    return gtmi_run_rows(db, (int)rows_b, 0, g, sc, stream);"""
     src = f"""// Generated by gt4py_amd (gt:mi355x). Do not edit.
 #include "gtmi_device.h"
 #include "gtmi.h"
@@ -129,18 +158,12 @@ extern "C" const char* gtmi_last_error(void) {{ return g_gtmi_err; }}
 extern "C" int gtmi_abi_version(void) {{ return GTMI_ABI_VERSION; }}
 extern "C" const char* gtmi_stencil_signature(void) {{ return "{sig_json}"; }}
 
-extern "C" int gtmi_stencil_run(const int64_t* domain, const gtmi_field* f, int32_t n_fields,
-                                const gtmi_scalar* sc, int32_t n_scalars, void* stream_ptr) {{
-    g_gtmi_err[0] = 0;
-    if (n_fields != {n_fields} || n_scalars != {n_scalars}) {{
-        snprintf(g_gtmi_err, sizeof(g_gtmi_err), "expected {n_fields} fields / {n_scalars} scalars, got %d / %d",
-                 (int)n_fields, (int)n_scalars);
-        return 1;
-    }}
+// Rows [0, jsplit) and [jsplit + jskip, nj) of the domain; an ordinary call has jsplit = nj.
+static int gtmi_run_rows(const int64_t* domain, int jsplit, int jskip, const gtmi_field* f, const gtmi_scalar* sc,
+                         hipStream_t stream) {{
     (void)sc; (void)f;
-    hipStream_t stream = (hipStream_t)stream_ptr;
     const int ni = (int)domain[0], nj = (int)domain[1], nk = (int)domain[2];
-    (void)ni; (void)nj; (void)nk;
+    (void)ni; (void)nj; (void)nk; (void)jsplit; (void)jskip;
     roctxRangePushA("{roctx_name}");  // ROCTX range around the launches (rocprofv3 --marker-trace)
 {chr(10).join(host_scalars)}
 {chr(10).join("    " + line for h in launches for line in h.splitlines())}
@@ -151,6 +174,36 @@ extern "C" int gtmi_stencil_run(const int64_t* domain, const gtmi_field* f, int3
         return (int)err;
     }}
     return 0;
+}}
+
+static int gtmi_check_counts(int32_t n_fields, int32_t n_scalars) {{
+    g_gtmi_err[0] = 0;
+    if (n_fields != {n_fields} || n_scalars != {n_scalars}) {{
+        snprintf(g_gtmi_err, sizeof(g_gtmi_err), "expected {n_fields} fields / {n_scalars} scalars, got %d / %d",
+                 (int)n_fields, (int)n_scalars);
+        return 1;
+    }}
+    return 0;
+}}
+
+extern "C" int gtmi_stencil_run(const int64_t* domain, const gtmi_field* f, int32_t n_fields,
+                                const gtmi_scalar* sc, int32_t n_scalars, void* stream_ptr) {{
+    if (int rc = gtmi_check_counts(n_fields, n_scalars)) return rc;
+    return gtmi_run_rows(domain, (int)domain[1], 0, f, sc, (hipStream_t)stream_ptr);
+}}
+
+extern "C" int gtmi_stencil_run_jsplit(const int64_t* domain, int64_t j_split, int64_t j_skip, const gtmi_field* f,
+                                       int32_t n_fields, const gtmi_scalar* sc, int32_t n_scalars, void* stream_ptr) {{
+    if (int rc = gtmi_check_counts(n_fields, n_scalars)) return rc;
+    if (j_split < 0 || j_skip < 0 || j_split + j_skip > domain[1]) {{
+        snprintf(g_gtmi_err, sizeof(g_gtmi_err), "bad row split %lld + %lld of %lld rows", (long long)j_split,
+                 (long long)j_skip, (long long)domain[1]);
+        return 1;
+    }}
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    const int64_t rows_b = domain[1] - j_split - j_skip;
+    if (j_split == 0 && rows_b == 0) return 0;
+{jsplit_body}
 }}
 """
     return src, signature

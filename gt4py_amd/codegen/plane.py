@@ -346,7 +346,7 @@ class PlaneGen:
                 L += ["    " + x for x in kparam_decl(s, s.name in written_slots)]
             for s in scalars:
                 L.append(f"    {s.dtype.ctype} s_{cname(s.name)};")
-            L.append("    int32_t ni, nj, nk, k0, nks, jc, n_strips, n_chunks, n_sgroups, perm_a;")
+            L.append("    int32_t ni, nj, nk, k0, nks, jc, n_strips, n_chunks, n_sgroups, perm_a, jsplit, jskip, ca;")
             L.append("};")
             L.append("")
         kname = f"k{k}_plane_v{V}"
@@ -398,8 +398,10 @@ class PlaneGen:
         B.append(f"const int strip = sg * {PLANE_BLOCK_WAVES} + wave;")
         B.append("if (strip >= p.n_strips) return;")
         B.append(f"const int ib = strip * {self.w_out};")
-        B.append("const int jb = chunk * p.jc;")
-        B.append("const int jce = min(p.jc, p.nj - jb);")
+        # rows [0, jsplit) and [jsplit + jskip, nj): chunks never straddle the gap (jsplit = nj and
+        # jskip = 0 for an ordinary call, gtmi_stencil_run_jsplit otherwise)
+        B.append("const int jb = chunk < p.ca ? chunk * p.jc : p.jsplit + p.jskip + (chunk - p.ca) * p.jc;")
+        B.append("const int jce = min(p.jc, (chunk < p.ca ? p.jsplit : p.nj) - jb);")
         B.append(f"const int w0 = ib - {self.h_lo};")
         B.append(f"const int pos = w0 + lane * {V};  // position of element 0 of this lane")
         for e in range(V):
@@ -586,7 +588,7 @@ class PlaneGen:
             H += ["        " + x for x in host_fill(s, "p", s.name in written_slots)]
         for i_s, s in enumerate(self.st.scalar_params()):
             H.append(f"        memcpy(&p.s_{cname(s.name)}, &sc[{i_s}], sizeof(p.s_{cname(s.name)}));")
-        H.append("        p.ni = ni; p.nj = nj; p.nk = nk; p.k0 = k0; p.nks = k1 - k0;")
+        H.append("        p.ni = ni; p.nj = nj; p.nk = nk; p.k0 = k0; p.nks = k1 - k0; p.jsplit = jsplit; p.jskip = jskip;")
         jchunk = int(self.opts.get("jchunk", 0))
         vecs = sorted(launches, reverse=True)
         H.append("        int vsel = 1;")
@@ -615,10 +617,11 @@ class PlaneGen:
                 # (MI355X sweeps: hdiff 2048^2x160 best at 16, lap5 1024^2x80 at 4, hdiff f32 at 16)
                 H.append("            p.jc = 32;")
                 H.append(
-                    f"            while (p.jc > {PLANE_MIN_JCHUNK} && (long long)p.n_sgroups * ((nj + p.jc - 1) / p.jc) * "
+                    f"            while (p.jc > {PLANE_MIN_JCHUNK} && (long long)p.n_sgroups * ((nj - jskip + p.jc - 1) / p.jc) * "
                     f"p.nks < {PLANE_TARGET_BLOCKS}LL) p.jc >>= 1;"
                 )
-            H.append("            p.n_chunks = (nj + p.jc - 1) / p.jc;")
+            H.append("            p.ca = (jsplit + p.jc - 1) / p.jc;  // chunks of the first row range")
+            H.append("            p.n_chunks = p.ca + (nj - jsplit - jskip + p.jc - 1) / p.jc;")
             if int(self.opts.get("order", 0)) == 5:  # per level: padded to a multiple of the 8 XCDs
                 H.append("            const long long nblocks = (long long)(((p.n_sgroups * p.n_chunks + 7) >> 3) * 8) * p.nks;")
             else:

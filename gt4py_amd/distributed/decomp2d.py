@@ -322,6 +322,16 @@ class HaloStencil2D:
         org = {k: (o[0] + i0, o[1] + j0, *o[2:]) for k, o in origin.items()}
         self.stencil(**kw, origin=org, domain=(ni, nj, nk), validate_args=False)
 
+    def _south_north(self, kw, origin, ni, nj, nk):
+        """The two full-width J bands, in one call over both row ranges when the stencil object
+        offers it (gt:mi355x: ``gtmi_stencil_run_jsplit``)."""
+        call_rows = getattr(self.stencil, "call_rows", None)
+        if call_rows is not None:
+            call_rows(self.hj, nj - 2 * self.hj, domain=(ni, nj, nk), origin=origin, validate_args=False, **kw)
+            return
+        for i0, j0, bi, bj in self.bands()[:2]:
+            self._run(kw, origin, i0, j0, bi, bj, nk)
+
     def band_width_i(self) -> int:
         """Width of the west/east bands. The halo width itself would leave bands a few columns
         wide, and a plane-kernel wave (one I strip of ~112-224 outputs) would then compute a
@@ -376,8 +386,7 @@ class HaloStencil2D:
                     self.ex.exchange_phase(fields, 1)
                 self._run(kw, origin, 0, hj, ni, nj - 2 * hj, nk)
                 main.wait_stream(self._stream)
-                for i0, j0, bi, bj in self.bands()[:2]:  # south and north, full width
-                    self._run(kw, origin, i0, j0, bi, bj, nk)
+                self._south_north(kw, origin, ni, nj, nk)
                 return
             with torch.cuda.stream(self._stream):
                 self.ex.exchange(fields)
@@ -391,8 +400,7 @@ class HaloStencil2D:
             pending = self.ex.start_phase(fields, 1)
             self._run(kw, origin, 0, hj, ni, nj - 2 * hj, nk)
             self.ex.finish_phase(pending)
-            for i0, j0, bi, bj in self.bands()[:2]:
-                self._run(kw, origin, i0, j0, bi, bj, nk)
+            self._south_north(kw, origin, ni, nj, nk)
             return
         else:
             # phase 0 (I faces) is packed and posted on the caller's stream, the interior runs

@@ -225,6 +225,7 @@ class HaloStencil:
         # computes the strips -- one cross-queue hand-off after the transfer instead of two
         # (+2.0-2.1 % vs +2.2-2.7 % per step)
         self.unpack_on_main = bands_on_halo is None and bands == "unpack_main"
+        self.fuse_strips = os.environ.get("GTMI_HALO_STRIPS", "fused") == "fused"
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
@@ -290,7 +291,13 @@ class HaloStencil:
         self._strips(kw, origin, ni, nj, nk)
 
     def _strips(self, kw, origin, ni, nj, nk):
+        """The two boundary strips: one call over both row ranges when the stencil object offers
+        it (gt:mi355x: one launch per kernel, ``gtmi_stencil_run_jsplit``), else two calls."""
         h = self.h
+        call_rows = getattr(self.stencil, "call_rows", None)
+        if call_rows is not None and self.fuse_strips:
+            call_rows(h, nj - 2 * h, domain=(ni, nj, nk), origin=origin, validate_args=False, **kw)
+            return
         self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
         self.stencil(**kw, origin=self._shifted(origin, nj - h), domain=(ni, h, nk), validate_args=False)
 

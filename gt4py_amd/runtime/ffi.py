@@ -12,7 +12,7 @@ import json
 import threading
 from typing import Dict
 
-GTMI_ABI_VERSION = 2
+GTMI_ABI_VERSION = 3
 
 DTYPE_IDS = {
     "bool": 10,
@@ -55,7 +55,8 @@ class GtmiScalar(ctypes.Union):
     ]
 
 
-EXPORTED_SYMBOLS = ("gtmi_stencil_run", "gtmi_stencil_signature", "gtmi_last_error", "gtmi_abi_version")
+EXPORTED_SYMBOLS = ("gtmi_stencil_run", "gtmi_stencil_run_jsplit", "gtmi_stencil_signature", "gtmi_last_error",
+                    "gtmi_abi_version")
 
 _libs: Dict[str, "StencilLibrary"] = {}
 _lock = threading.Lock()
@@ -77,6 +78,9 @@ class StencilLibrary:
             ctypes.c_int32,
             ctypes.c_void_p,
         ]
+        self.run_jsplit = self.lib.gtmi_stencil_run_jsplit
+        self.run_jsplit.restype = ctypes.c_int
+        self.run_jsplit.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.c_int64] + self.run.argtypes[1:]
         self.lib.gtmi_last_error.restype = ctypes.c_char_p
         self.lib.gtmi_stencil_signature.restype = ctypes.c_char_p
         self.lib.gtmi_abi_version.restype = ctypes.c_int

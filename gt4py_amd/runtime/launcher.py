@@ -198,7 +198,9 @@ class StencilLauncher:
         return fields, device, refs, ptrs
 
     def __call__(self, domain, origin, arrays: Dict[str, Any], params: Dict[str, Any], *, device_sync=True,
-                 exec_info=None) -> None:
+                 exec_info=None, rows=None) -> None:
+        """``rows=(j_split, j_skip)``: only rows [0, j_split) and [j_split + j_skip, nj) of ``domain``
+        (``gtmi_stencil_run_jsplit``)."""
         import torch
 
         lib = self.lib
@@ -216,18 +218,22 @@ class StencilLauncher:
         dom = (ctypes.c_int64 * 3)(ni, nj, nk)
         if device.index is not None and device.index != torch.cuda.current_device():
             with torch.cuda.device(device):
-                self._run(lib, dom, fields, scalars, n_sc, device, device_sync, exec_info)
+                self._run(lib, dom, fields, scalars, n_sc, device, device_sync, exec_info, rows)
         else:
-            self._run(lib, dom, fields, scalars, n_sc, device, device_sync, exec_info)
+            self._run(lib, dom, fields, scalars, n_sc, device, device_sync, exec_info, rows)
 
-    def _run(self, lib, dom, fields, scalars, n_sc, device, device_sync, exec_info):
+    def _run(self, lib, dom, fields, scalars, n_sc, device, device_sync, exec_info, rows=None):
         import torch
 
         stream = torch.cuda.current_stream(device)
         if exec_info is not None:
             stream.synchronize()
             exec_info["run_cpp_start_time"] = time.perf_counter()
-        rc = lib.run(dom, fields, self.n_fields, scalars, n_sc, ctypes.c_void_p(stream.cuda_stream))
+        if rows is None:
+            rc = lib.run(dom, fields, self.n_fields, scalars, n_sc, ctypes.c_void_p(stream.cuda_stream))
+        else:
+            rc = lib.run_jsplit(dom, int(rows[0]), int(rows[1]), fields, self.n_fields, scalars, n_sc,
+                                ctypes.c_void_p(stream.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"gt:mi355x stencil '{self.name}' failed: {lib.last_error()}")
         if device_sync or exec_info is not None:

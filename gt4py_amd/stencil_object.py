@@ -368,7 +368,18 @@ class StencilObject(abc.ABC):
                 origin[name] = (0,) * field_info.ndim
         return origin
 
-    def _call_run(self, field_args, parameter_args, domain, origin, *, validate_args=True, exec_info=None):
+    def call_rows(self, j_split: int, j_skip: int, *, domain, origin, validate_args=True, exec_info=None, **kwargs):
+        """Run over the rows ``[0, j_split)`` and ``[j_split + j_skip, nj)`` of ``domain`` only (a
+        gt4py_amd extension, no reference counterpart): the two boundary strips of a J-strip rank
+        after its halo exchange (``distributed/halo.py``). gt:mi355x computes both in one launch
+        per kernel when it can (``gtmi_stencil_run_jsplit``, include/gtmi.h); other backends make
+        two calls. Arguments as ``__call__``; ``domain`` is the full (ni, nj, nk) region."""
+        field_args = {n: kwargs.get(n) for n in self.field_info}
+        parameter_args = {n: kwargs.get(n) for n in self.parameter_info}
+        self._call_run(field_args, parameter_args, domain, origin, validate_args=validate_args, exec_info=exec_info,
+                       rows=(int(j_split), int(j_skip)))
+
+    def _call_run(self, field_args, parameter_args, domain, origin, *, validate_args=True, exec_info=None, rows=None):
         if exec_info is not None:
             exec_info["call_run_start_time"] = time.perf_counter()
         from gt4py_amd.backend import from_name
@@ -387,9 +398,38 @@ class StencilObject(abc.ABC):
         else:
             domain, origin = cache[cache_key]
         arrays = {name: (info.array if info is not None else None) for name, info in array_infos.items()}
-        self.run(_domain_=domain, _origin_=origin, exec_info=exec_info, **arrays, **parameter_args)
+        if rows is None:
+            self.run(_domain_=domain, _origin_=origin, exec_info=exec_info, **arrays, **parameter_args)
+        else:
+            self._run_rows(domain, origin, exec_info, arrays, parameter_args, *rows)
         if exec_info is not None:
             exec_info["call_run_end_time"] = time.perf_counter()
+
+    def _run_rows(self, domain, origin, exec_info, arrays, parameter_args, j_split, j_skip):
+        ni, nj, nk = domain
+        if j_split < 0 or j_skip < 0 or j_split + j_skip > nj:
+            raise ValueError(f"row split {j_split} + {j_skip} does not fit {nj} rows")
+        impl = type(self)._gt_run_impl_
+        if getattr(impl, "supports_rows", False):
+            if exec_info is not None:
+                exec_info["domain"], exec_info["origin"] = domain, origin
+                exec_info["run_start_time"] = time.perf_counter()
+            impl(domain, origin, exec_info, {**arrays, **parameter_args}, rows=(j_split, j_skip))
+            if exec_info is not None:
+                exec_info["run_end_time"] = time.perf_counter()
+            return
+        if j_split > 0:
+            self.run(_domain_=(ni, j_split, nk), _origin_=origin, exec_info=exec_info, **arrays, **parameter_args)
+        rows_b = nj - j_split - j_skip
+        if rows_b > 0:
+            shifted = {}
+            for name, org in origin.items():
+                axes = self.field_info[name].axes if name in self.field_info and self.field_info[name] else ()
+                if "J" in axes:
+                    q = list(axes).index("J")
+                    org = tuple(o + (j_split + j_skip if d == q else 0) for d, o in enumerate(org))
+                shifted[name] = org
+            self.run(_domain_=(ni, rows_b, nk), _origin_=shifted, exec_info=exec_info, **arrays, **parameter_args)
 
     def freeze(self, *, origin: Dict[str, Tuple[int, ...]], domain: Tuple[int, ...]) -> FrozenStencil:
         return FrozenStencil(self, origin, domain)

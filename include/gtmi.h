@@ -2,7 +2,7 @@
  * gtmi.h -- C ABI of gt:mi355x generated stencil libraries.
  *
  * Every stencil built by the gt:mi355x backend is one shared library (hipcc, gfx950) that
- * exports exactly the four entry points below. They replace the pybind11 extension that the
+ * exports exactly the five entry points below. They replace the pybind11 extension that the
  * reference's GridTools backends generate per stencil:
  *
  *   reference: backend/gtc_common.py:65-103  (bindings_main_template)
@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GTMI_ABI_VERSION 2
+#define GTMI_ABI_VERSION 3
 #define GTMI_MAX_DATA_DIMS 4
 
 /* dtype ids = gt4py DataType ids (gtc/common.py:105-118) */
@@ -75,6 +75,16 @@ typedef union gtmi_scalar {
  * scratch temporaries listed in gtmi_stencil_signature(). Returns 0 on success. */
 int gtmi_stencil_run(const int64_t* domain, const gtmi_field* fields, int32_t n_fields,
                      const gtmi_scalar* scalars, int32_t n_scalars, void* stream);
+
+/* gtmi_stencil_run over the rows [0, j_split) and [j_split + j_skip, domain[1]) of `domain`
+ * only; the rows in between are not touched. One launch per kernel when every kernel of the
+ * stencil is a plane kernel without scratch temporaries or horizontal regions, otherwise two
+ * passes (the second with every field's J origin advanced by j_split + j_skip).
+ * No reference counterpart: the reference has no multi-device path (users cut the domain by
+ * hand through origin/domain, stencil_object.py:155-175); this serves the two boundary strips
+ * of a J-strip rank after its halo exchange (gt4py_amd/distributed/halo.py). */
+int gtmi_stencil_run_jsplit(const int64_t* domain, int64_t j_split, int64_t j_skip, const gtmi_field* fields,
+                            int32_t n_fields, const gtmi_scalar* scalars, int32_t n_scalars, void* stream);
 
 /* JSON description: {"abi":1,"fields":[...],"scratch":[...],"scalars":[...],"kernels":[...]} */
 const char* gtmi_stencil_signature(void);

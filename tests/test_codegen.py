@@ -83,9 +83,9 @@ def test_library_loads_and_describes_itself(name):
     stencil = gtscript.stencil(backend="gt:mi355x", definition=case.definition, externals=case.externals,
                                name=f"gpu.{name}")
     lib = ffi.load_library(_lib_path(stencil))
-    assert lib.lib.gtmi_abi_version() == ffi.GTMI_ABI_VERSION == 2
+    assert lib.lib.gtmi_abi_version() == ffi.GTMI_ABI_VERSION == 3
     sig = lib.signature
-    assert sig["abi"] == 2
+    assert sig["abi"] == 3
     assert [f["name"] for f in sig["fields"]] == list(stencil.field_info.keys())
     for f in sig["fields"]:
         fi = stencil.field_info[f["name"]]
