@@ -15,8 +15,9 @@ Timing: W untimed warmups, then K steps bracketed by barrier + synchronize; max 
 ``roofline`` = algorithmic bytes (24 B/cell: in + coeff read, out written)
 per launch / mean launch time from HIP events on the launch stream; ``traffic`` = rocprofv3
 PMC bytes per launch from ``profiles/pmc_<config>.json`` when that record was measured on the
-same library (build key), else null. ``extra_configs`` (N=1): the other BASELINE configs timed
-in the same process. ``cpu_baseline`` = the C restatement (cpu_ifirst-equivalent, OpenMP) on
+same library (build key), else null. ``sustained`` (N=1): the same step repeated for ~3 s after
+the timed K steps (steady-state ms/step; ``--sustain 0`` skips it). ``extra_configs`` (N=1): the
+other BASELINE configs timed in the same process. ``cpu_baseline`` = the C restatement (cpu_ifirst-equivalent, OpenMP) on
 the full domain, median of 20 after 3 warm-ups, in a child process.
 """
 
@@ -525,6 +526,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="N=1: skip the extra_configs timings")
     ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--sustain", type=float, default=3.0,
+                    help="N=1: after the timed K steps, run the step for about this many seconds more and report "
+                         "the steady-state ms/step as `sustained` (0 = off)")
     ap.add_argument("--jchunk", type=int, default=None)
     ap.add_argument("--opt", action="append", default=None, metavar="KEY=VALUE",
                     help="gt:mi355x codegen option for the headline config (repeatable)")
@@ -661,6 +665,15 @@ def main():
     }
     if halo_ab is not None:
         result["halo_ab"] = halo_ab
+    if world == 1 and not args.dry_run and not args.halo_selfcomm and args.sustain > 0:
+        # steady state over seconds rather than tens of milliseconds (clocks, HBM refresh, the
+        # driver's utilisation sampler); the headline `value` stays the K-step measurement
+        n_s = max(args.steps, int(args.sustain / max(elapsed / args.steps, 1e-6)))
+        el_s, _ = time_workload(wl, n_s, 0, dev, None, events=False)
+        ms_s = el_s / n_s * 1e3
+        result["sustained"] = {"steps": n_s, "seconds": round(el_s, 2), "ms_per_step": round(ms_s, 4),
+                               "Mcells_s": round(cells_per_step / (ms_s * 1e-3) / 1e6, 1),
+                               "frac": round(cells_per_step * wl.bpc / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     if args.dry_run:
         result["dry_run"] = True
         result["data"] = "synthetic; DRY RUN on CPU (numpy backend, gloo): not a measurement"
