@@ -16,7 +16,8 @@ Timing: W untimed warmups, then K steps bracketed by barrier + synchronize; max 
 per launch / mean launch time from HIP events on the launch stream; ``traffic`` = rocprofv3
 PMC bytes per launch from ``profiles/pmc_<config>.json`` when that record was measured on the
 same library (build key), else null. ``sustained`` (N=1): the same step repeated for ~3 s after
-the timed K steps (steady-state ms/step; ``--sustain 0`` skips it). ``extra_configs`` (N=1): the
+the timed K steps (steady-state ms/step; ``--sustain 0`` skips it). ``full_call`` (N=1): K calls
+the reference's way (validate_args=True, synchronize after each). ``extra_configs`` (N=1): the
 other BASELINE configs timed in the same process. ``cpu_baseline`` = the C restatement (cpu_ifirst-equivalent, OpenMP) on
 the full domain, median of 20 after 3 warm-ups, in a child process.
 """
@@ -304,6 +305,7 @@ class Workload:
         from gt4py_amd.distributed import Decomposition2D, HaloStencil, HaloStencil2D
 
         self.cfg = cfg
+        self.dev = dev
         sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[cfg]
         if dry_run:  # CPU rehearsal of the launcher / rendezvous / halo path: a small tile per rank
             ni, nj, nk = 64, 32, 8
@@ -398,6 +400,15 @@ class Workload:
             self.halo(self.named, self.origin, self.domain)
         else:
             self.plain_step()
+
+    def validated_step(self):
+        """The reference's default call: full argument validation (cached per domain/origin
+        signature, as the reference's ``_domain_origin_cache``) and synchronisation after the call."""
+        self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain, validate_args=True)
+        if self.dev.type == "cuda":
+            import torch
+
+            torch.cuda.synchronize()
 
     def plain_step(self):
         """One launch over the whole local domain, no exchange (the halo path's A/B reference)."""
@@ -674,6 +685,13 @@ def main():
         result["sustained"] = {"steps": n_s, "seconds": round(el_s, 2), "ms_per_step": round(ms_s, 4),
                                "Mcells_s": round(cells_per_step / (ms_s * 1e-3) / 1e6, 1),
                                "frac": round(cells_per_step * wl.bpc / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if world == 1 and not args.dry_run and not args.halo_selfcomm:
+        # full-call time: validate_args=True and a synchronize after every call,
+        # i.e. host validation + launch + kernel + sync, as a plain reference-style call loop
+        el_v, _ = time_workload(wl, args.steps, 1, dev, None, events=False, step=wl.validated_step)
+        result["full_call"] = {"validate_args": True, "sync_each_call": True,
+                               "ms_per_call": round(el_v / args.steps * 1e3, 4),
+                               "host_overhead_ms": round(el_v / args.steps * 1e3 - (kernel_ms or 0.0), 4)}
     if args.dry_run:
         result["dry_run"] = True
         result["data"] = "synthetic; DRY RUN on CPU (numpy backend, gloo): not a measurement"
