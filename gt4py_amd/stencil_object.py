@@ -374,6 +374,9 @@ class StencilObject(abc.ABC):
         after its halo exchange (``distributed/halo.py``). gt:mi355x computes both in one launch
         per kernel when it can (``gtmi_stencil_run_jsplit``, include/gtmi.h); other backends make
         two calls. Arguments as ``__call__``; ``domain`` is the full (ni, nj, nk) region."""
+        unknown = sorted(set(kwargs) - set(self.field_info) - set(self.parameter_info))
+        if unknown:
+            raise TypeError(f"call_rows() got unexpected keyword argument(s) {unknown}")
         field_args = {n: kwargs.get(n) for n in self.field_info}
         parameter_args = {n: kwargs.get(n) for n in self.parameter_info}
         self._call_run(field_args, parameter_args, domain, origin, validate_args=validate_args, exec_info=exec_info,

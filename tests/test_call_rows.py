@@ -101,6 +101,8 @@ def test_call_rows_rejects_bad_split():
     host, origin, (ni, nj, nk) = _setup(case, st)
     with pytest.raises(ValueError):
         st.call_rows(nj, 1, domain=(ni, nj, nk), origin=origin, **host)
+    with pytest.raises(TypeError):
+        st.call_rows(1, 1, domain=(ni, nj, nk), origin=origin, not_a_field=host["field_a"], **host)
 
 
 @pytest.mark.parametrize("name,path", [c for c in CASES if c[1] is not None])
