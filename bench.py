@@ -48,6 +48,11 @@ CONFIGS = {
     "vadv": ("vertical_advection_dycore", np.float64, (1024, 1024, 160), 0, 48),
     # hdiff written as three computations (lap / fluxes / update): fused into one launch
     "hdiff_blocks": ("horizontal_diffusion_blocks", np.float64, (2048, 2048, 160), 2, 24),
+    # shape probes for work-order experiments (scripts/sweep.py; never bench lines)
+    "lap5_k160": ("lap5", np.float64, (1024, 1024, 160), 1, 16),
+    "lap5_2k": ("lap5", np.float64, (2048, 2048, 80), 1, 16),
+    "copy_k80": ("copy_stencil", np.float64, (1024, 1024, 80), 0, 16),
+    "hdiff_k80": ("horizontal_diffusion", np.float64, (2048, 2048, 80), 2, 24),
 }
 
 

@@ -90,7 +90,7 @@ class Mi355xBackend(BaseBackend):
         "strip_align": {"versioning": True, "type": int, "description": "round plane-strip width to a multiple"},
         "min_blocks": {"versioning": True, "type": int, "description": "plane kernels: __launch_bounds__ min blocks per CU"},
         "pointwise_plane": {"versioning": True, "type": int, "description": "stream pointwise PARALLEL loops with K1"},
-        "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow, 5 level-synchronous xcd)"},
+        "order": {"versioning": True, "type": int, "description": "plane work order (0 xcd, 1 k-fast, 2 scatter, 3 natural, 4 chunk-slow, 5 level-synchronous xcd, 6 auto: 5 for small launches else 0, default)"},
         "nt_store": {"versioning": True, "type": int, "description": "non-temporal stores of API fields"},
         "nt_load": {"versioning": True, "type": int, "description": "non-temporal loads of read-once streams"},
         "kring": {"versioning": True, "type": int, "description": "column kernels: window-front loads in flight (levels)"},

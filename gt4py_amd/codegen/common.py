@@ -17,6 +17,9 @@ WAVE = 64
 PLANE_BLOCK_WAVES = 4
 PLANE_TARGET_BLOCKS = 60000  # auto J-chunk: aim for at least this many workgroups
 PLANE_MIN_JCHUNK = 4
+PLANE_ORDER_AUTO = 6  # plane work order chosen per launch: level-synchronous (5) for small launches, else XCD ranges (0)
+PLANE_LVLSYNC_MAX_PLANE = 1 << 20  # ... when the plane has at most this many cells
+PLANE_LVLSYNC_MAX_LEVELS = 80  # ... and the launch at most this many levels
 COLUMN_BLOCK = (64, 4)
 
 

@@ -14,7 +14,7 @@ from gt4py_amd.codegen.plan import ColumnKernel, KernelPlan, PlaneKernel, Unsupp
 from gt4py_amd.ir import DataType
 from gt4py_amd.passes import ZERO_EXTENT, StencilAnalysis, iter_accesses
 from gt4py_amd.codegen.common import (  # noqa: F401
-    COLUMN_BLOCK, PLANE_BLOCK_WAVES, PLANE_MIN_JCHUNK, PLANE_TARGET_BLOCKS, WAVE, ExprRenderer, FieldSlot, cname,
+    COLUMN_BLOCK, PLANE_BLOCK_WAVES, PLANE_LVLSYNC_MAX_LEVELS, PLANE_LVLSYNC_MAX_PLANE, PLANE_MIN_JCHUNK, PLANE_ORDER_AUTO, PLANE_TARGET_BLOCKS, WAVE, ExprRenderer, FieldSlot, cname,
     host_fill, interval_bounds, kparam_decl, literal, region_condition,
 )
 
@@ -346,7 +346,7 @@ class PlaneGen:
                 L += ["    " + x for x in kparam_decl(s, s.name in written_slots)]
             for s in scalars:
                 L.append(f"    {s.dtype.ctype} s_{cname(s.name)};")
-            L.append("    int32_t ni, nj, nk, k0, nks, jc, n_strips, n_chunks, n_sgroups, perm_a, jsplit, jskip, ca;")
+            L.append("    int32_t ni, nj, nk, k0, nks, jc, n_strips, n_chunks, n_sgroups, perm_a, jsplit, jskip, ca, lvlsync;")
             L.append("};")
             L.append("")
         kname = f"k{k}_plane_v{V}"
@@ -356,45 +356,62 @@ class PlaneGen:
         B = []
         B.append("const int lane = (int)__lane_id();")
         B.append("const int wave = (int)(threadIdx.x >> 6);")
-        order = int(self.opts.get("order", 0))
+        order = int(self.opts.get("order", PLANE_ORDER_AUTO))
         B.append("const int nb = (int)gridDim.x, b = (int)blockIdx.x;")
-        if order == 3:
-            B.append("const int w = b;  // natural dispatch order")
-        elif order == 5:
+
+        def lvlsync():
             # level-synchronous XCD-aware order: every level's work items are cut into 8 contiguous
             # ranges, one per XCD (blocks are dispatched round-robin over the XCDs), so all XCDs
             # stream the same few levels at a time while each keeps its neighbours in its own L2
-            B.append("const int per_lvl = p.n_sgroups * p.n_chunks, m8 = (per_lvl + 7) >> 3;")
-            B.append("const int lvl = b / (m8 * 8), loc = b - lvl * m8 * 8;")
-            B.append("const int w = (loc & 7) * m8 + (loc >> 3);")
-            B.append("if (w >= per_lvl) return;  // padding block (whole workgroup)")
-        else:
-            B.append("// XCD-aware block remap: consecutive work items share an XCD (8 XCDs, round-robin dispatch)")
-            B.append("const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;")
-            B.append("const int w0x = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;")
-            if order == 2:
-                B.append("const int w = (int)(((long long)w0x * p.perm_a) % nb);  // bijective scatter")
+            return [
+                "const int per_lvl = p.n_sgroups * p.n_chunks, m8 = (per_lvl + 7) >> 3;",
+                "const int lvl = b / (m8 * 8), loc = b - lvl * m8 * 8;",
+                "const int w = (loc & 7) * m8 + (loc >> 3);",
+                "if (w >= per_lvl) return;  // padding block (whole workgroup)",
+                "sg = w % p.n_sgroups;",
+                "chunk = w / p.n_sgroups;",
+                "kk = p.k0 + lvl;",
+            ]
+
+        def xcd_ranges(o):
+            L2 = [
+                "// XCD-aware block remap: consecutive work items share an XCD (8 XCDs, round-robin dispatch)",
+                "const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;",
+                "const int w0x = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;",
+            ]
+            if o == 3:
+                L2 = ["const int w = b;  // natural dispatch order"]
+            elif o == 2:
+                L2.append("const int w = (int)(((long long)w0x * p.perm_a) % nb);  // bijective scatter")
             else:
-                B.append("const int w = w0x;")
+                L2.append("const int w = w0x;")
+            if o == 4:  # chunks slowest: chunk c+1 starts as chunk c ends on the same XCD (halo rows warm)
+                L2 += ["sg = w % p.n_sgroups;", "const int rest = w / p.n_sgroups;", "kk = p.k0 + rest % p.nks;",
+                       "chunk = rest / p.nks;"]
+            elif o == 1:
+                L2 += ["kk = p.k0 + w % p.nks;", "const int rest = w / p.nks;", "sg = rest % p.n_sgroups;",
+                       "chunk = rest / p.n_sgroups;"]
+            else:
+                L2 += ["sg = w % p.n_sgroups;", "const int rest = w / p.n_sgroups;", "chunk = rest % p.n_chunks;",
+                       "kk = p.k0 + rest / p.n_chunks;"]
+            return L2
+
+        B.append("int sg, chunk, kk;")
         if order == 5:
-            B.append("const int sg = w % p.n_sgroups;")
-            B.append("const int chunk = w / p.n_sgroups;")
-            B.append("const int kk = p.k0 + lvl;")
-        elif order == 4:  # chunks slowest: chunk c+1 starts as chunk c ends on the same XCD (halo rows warm)
-            B.append("const int sg = w % p.n_sgroups;")
-            B.append("const int rest = w / p.n_sgroups;")
-            B.append("const int kk = p.k0 + rest % p.nks;")
-            B.append("const int chunk = rest / p.nks;")
-        elif order == 1:
-            B.append("const int kk = p.k0 + w % p.nks;")
-            B.append("const int rest = w / p.nks;")
-            B.append("const int sg = rest % p.n_sgroups;")
-            B.append("const int chunk = rest / p.n_sgroups;")
+            B.append("{")
+            B += ["    " + x for x in lvlsync()]
+            B.append("}")
+        elif order == PLANE_ORDER_AUTO:
+            # chosen per launch by the host (p.lvlsync, see _render_host): uniform branch
+            B.append("if (p.lvlsync) {")
+            B += ["    " + x for x in lvlsync()]
+            B.append("} else {")
+            B += ["    " + x for x in xcd_ranges(0)]
+            B.append("}")
         else:
-            B.append("const int sg = w % p.n_sgroups;")
-            B.append("const int rest = w / p.n_sgroups;")
-            B.append("const int chunk = rest % p.n_chunks;")
-            B.append("const int kk = p.k0 + rest / p.n_chunks;")
+            B.append("{")
+            B += ["    " + x for x in xcd_ranges(order)]
+            B.append("}")
         B.append(f"const int strip = sg * {PLANE_BLOCK_WAVES} + wave;")
         B.append("if (strip >= p.n_strips) return;")
         B.append(f"const int ib = strip * {self.w_out};")
@@ -622,10 +639,21 @@ class PlaneGen:
                 )
             H.append("            p.ca = (jsplit + p.jc - 1) / p.jc;  // chunks of the first row range")
             H.append("            p.n_chunks = p.ca + (nj - jsplit - jskip + p.jc - 1) / p.jc;")
-            if int(self.opts.get("order", 0)) == 5:  # per level: padded to a multiple of the 8 XCDs
-                H.append("            const long long nblocks = (long long)(((p.n_sgroups * p.n_chunks + 7) >> 3) * 8) * p.nks;")
+            order = int(self.opts.get("order", PLANE_ORDER_AUTO))
+            if order == PLANE_ORDER_AUTO:
+                # level-synchronous order for small launches: measured faster for planes of <= 1M
+                # cells over <= 80 levels (lap5 1024^2x80 +3.5 %, copy 1024^2x80 +4.6 %), slower or
+                # mixed beyond (hdiff 2048^2x80 -1 %, lap5 2048^2x80 -0.4 %, copy 1024^2x160 -1.3 to
+                # +2.5 %, hdiff 2048^2x160 -1 to -8.5 %): profiles/r02z_sweep_order_shapes.log
+                H.append(
+                    f"            p.lvlsync = ((long long)ni * nj <= {PLANE_LVLSYNC_MAX_PLANE}LL && p.nks <= "
+                    f"{PLANE_LVLSYNC_MAX_LEVELS}) ? 1 : 0;"
+                )
             else:
-                H.append("            const long long nblocks = (long long)p.n_sgroups * p.n_chunks * p.nks;")
+                H.append(f"            p.lvlsync = {1 if order == 5 else 0};")
+            H.append("            const long long nblocks = p.lvlsync  // per level: padded to a multiple of the 8 XCDs")
+            H.append("                ? (long long)(((p.n_sgroups * p.n_chunks + 7) >> 3) * 8) * p.nks")
+            H.append("                : (long long)p.n_sgroups * p.n_chunks * p.nks;")
             H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); roctxRangePop(); return 2; }")
             H.append("            p.perm_a = gtmi_coprime_multiplier((long long)nblocks);")
             H.append(
