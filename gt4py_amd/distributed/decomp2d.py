@@ -98,13 +98,16 @@ def _backend_name(group=None) -> str:
 
 
 class HaloExchange2D:
-    """Two-phase, batched halo exchange of ``[ni+2hi, nj+2hj, nk]`` fields."""
+    """Batched halo exchange of ``[ni+2hi, nj+2hj, nk]`` fields: two phases (I faces, then J
+    faces over the full width), or with ``diagonal=True`` ONE phase that also sends the four
+    corner boxes to the diagonal neighbours (8 messages, one pack, one unpack)."""
 
     def __init__(self, decomp: Decomposition2D, rank: int, halo: Tuple[int, int], group=None,
-                 force_comm: bool = False):
+                 force_comm: bool = False, diagonal: bool = False):
         """``force_comm``: send to oneself through the communicator instead of copying locally
         (a periodic axis with one rank); lets one GPU exercise the RCCL path end to end."""
         self.force_comm = force_comm
+        self.diagonal = diagonal
         self.d = decomp
         self.rank = rank
         self.hi, self.hj = halo
@@ -117,6 +120,9 @@ class HaloExchange2D:
             "S": decomp.rank_of(ci, cj - 1) if self.hj else None,
             "N": decomp.rank_of(ci, cj + 1) if self.hj else None,
         }
+        both = bool(self.hi and self.hj)
+        for d, (dx, dy) in (("SW", (-1, -1)), ("SE", (1, -1)), ("NW", (-1, 1)), ("NE", (1, 1))):
+            self.nbr[d] = decomp.rank_of(ci + dx, cj + dy) if both else None
         self._host = None
         self._copies: Dict[Tuple, Tuple] = {}
         self._bufs: Dict[Tuple, object] = {}
@@ -133,13 +139,33 @@ class HaloExchange2D:
                 "W": ((slice(hi, 2 * hi), js), (slice(0, hi), js)),
                 "E": ((slice(ni, ni + hi), js), (slice(ni + hi, ni + 2 * hi), js)),
             }
-        is_ = slice(0, ni + 2 * hi)  # J faces over the full width: corners travel along
+        if phase == 1:
+            is_ = slice(0, ni + 2 * hi)  # J faces over the full width: corners travel along
+            return {
+                "S": ((is_, slice(hj, 2 * hj)), (is_, slice(0, hj))),
+                "N": ((is_, slice(nj, nj + hj)), (is_, slice(nj + hj, nj + 2 * hj))),
+            }
+        # phase 2 = the single diagonal phase: faces over the interior, extended over the halo of
+        # a global (non-periodic) boundary of the other axis, whose corner no diagonal rank owns
+        nb = self.nbr
+        js = slice(0 if nb["S"] is None else hj, hj + nj + (hj if nb["N"] is None else 0))
+        is_ = slice(0 if nb["W"] is None else hi, hi + ni + (hi if nb["E"] is None else 0))
+        lo_i, hi_i = slice(hi, 2 * hi), slice(ni, ni + hi)  # sent: first / last interior columns
+        lo_j, hi_j = slice(hj, 2 * hj), slice(nj, nj + hj)
+        hw, he = slice(0, hi), slice(ni + hi, ni + 2 * hi)  # received: west / east halo columns
+        hs, hn = slice(0, hj), slice(nj + hj, nj + 2 * hj)
         return {
-            "S": ((is_, slice(hj, 2 * hj)), (is_, slice(0, hj))),
-            "N": ((is_, slice(nj, nj + hj)), (is_, slice(nj + hj, nj + 2 * hj))),
+            "W": ((lo_i, js), (hw, js)),
+            "E": ((hi_i, js), (he, js)),
+            "S": ((is_, lo_j), (is_, hs)),
+            "N": ((is_, hi_j), (is_, hn)),
+            "SW": ((lo_i, lo_j), (hw, hs)),
+            "SE": ((hi_i, lo_j), (he, hs)),
+            "NW": ((lo_i, hi_j), (hw, hn)),
+            "NE": ((hi_i, hi_j), (he, hn)),
         }
 
-    _OPPOSITE = {"W": "E", "E": "W", "S": "N", "N": "S"}
+    _OPPOSITE = {"W": "E", "E": "W", "S": "N", "N": "S", "SW": "NE", "NE": "SW", "SE": "NW", "NW": "SE"}
 
     def _buffer(self, key, numel, like):
         import torch
@@ -177,12 +203,13 @@ class HaloExchange2D:
                     face = t[faces[d][0][0], faces[d][0][1], :]
                     sbuf[d][off : off + n].view(face.shape).copy_(face)
                     off += n
-        # my d-halo receives the neighbour's opposite face. Sends are posted in the opposite
-        # order of the receives, so that with two ranks on a periodic axis (W and E are the same
-        # peer) the k-th receive from a peer matches that peer's k-th send.
+        # my d-halo receives the neighbour's opposite face. Receives are posted in the canonical
+        # direction order, sends toward opposite(d) in the same order: a peer that is my
+        # neighbour in several directions (two ranks on a periodic axis) then matches its k-th
+        # send to me with my k-th receive from it (neighbourhood is symmetric).
         ops, unpack = [], []
         local = lambda peer: peer == self.rank and not self.force_comm  # noqa: E731
-        for d in reversed(dirs):
+        for d in [self._OPPOSITE[x] for x in faces if self._OPPOSITE[x] in dirs]:
             peer = self.nbr[d]
             if not local(peer):
                 gpeer = dist.get_global_rank(self.group, peer) if self.group is not None else peer
@@ -254,8 +281,11 @@ class HaloExchange2D:
         if not fields:
             return
         for group in self._groups(fields):
-            self._phase(group, 0)
-            self._phase(group, 1)
+            if self.diagonal:
+                self._phase(group, 2)
+            else:
+                self._phase(group, 0)
+                self._phase(group, 1)
 
     def exchange_phase(self, fields: Sequence, phase: int) -> None:
         """Only phase ``phase`` (0: I faces, 1: J faces incl. corners) of every dtype group."""
@@ -294,13 +324,22 @@ class HaloStencil2D:
 
     def __init__(self, stencil, halo_fields: Sequence[str], decomp: Decomposition2D, rank: int,
                  halo: Tuple[int, int], group=None, overlap: bool = True, force_comm: bool = False,
-                 stream_mode: Optional[str] = None, ifirst: Optional[bool] = None):
+                 stream_mode: Optional[str] = None, ifirst: Optional[bool] = None, scheme: Optional[str] = None):
         """``ifirst`` (default ``GTMI_HALO2D_IFIRST``, on): exchange the I faces
         before the interior, which then spans the full I width and overlaps only the J-face
         phase; off: the interior excludes west/east bands that run after both phases."""
         self.stencil = stencil
         self.halo_fields = list(halo_fields)
-        self.ex = HaloExchange2D(decomp, rank, halo, group, force_comm=force_comm)
+        # "two_phase" (default, GTMI_HALO2D_SCHEME): I faces then J faces, overlapped as below;
+        # "diagonal": one exchange phase with corner messages to the diagonal neighbours, then the
+        # whole tile in one launch -- measured slower on MI355X (+7.9-8.2 % vs +6.5 %): RCCL splits
+        # the 16-operation group into three kernels and starts it ~100 us after the pack
+        # (DESIGN.md §6)
+        self.scheme = scheme or os.environ.get("GTMI_HALO2D_SCHEME", "two_phase")
+        if self.scheme not in ("diagonal", "two_phase"):
+            raise ValueError(f"scheme must be 'diagonal' or 'two_phase', got {self.scheme!r}")
+        self.ex = HaloExchange2D(decomp, rank, halo, group, force_comm=force_comm,
+                                 diagonal=self.scheme == "diagonal")
         self.hi, self.hj = halo
         self.ni, self.nj = decomp.local_shape(rank)
         self.overlap = (
@@ -361,7 +400,10 @@ class HaloStencil2D:
         fields = [args[n] for n in self.halo_fields]
         kw = dict(args)
         kw.update(params)
-        if not self.overlap:
+        if not self.overlap or self.scheme == "diagonal":
+            # diagonal: the exchange is one pack, one RCCL group, one unpack; overlapping it buys
+            # nothing while RCCL's kernel waits for CUs behind the interior (measured for the
+            # two-phase scheme: overlapped +6.1-6.5 %, not overlapped +6.4-6.8 %)
             self.ex.exchange(fields)
             self.stencil(**kw, origin=origin, domain=domain, validate_args=False)
             return

@@ -116,7 +116,7 @@ def test_jstrips_cover_domain():
 # ---------------------------------------------------------------------------------------
 
 
-def _worker2d(rank, world, port, outdir, pi, pj, periodic, ifirst=True):
+def _worker2d(rank, world, port, outdir, pi, pj, periodic, ifirst=True, scheme="two_phase"):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -152,7 +152,7 @@ def _worker2d(rank, world, port, outdir, pi, pj, periodic, ifirst=True):
     st = gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist2d.hdiff")
     args = {"in_field": t_in, "out_field": t_out, "coeff": torch.from_numpy(gco[i0:i1, j0:j1, :].copy())}
     origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
-    runner = HaloStencil2D(st, ["in_field"], dec, rank, (h, h), ifirst=ifirst)
+    runner = HaloStencil2D(st, ["in_field"], dec, rank, (h, h), ifirst=ifirst, scheme=scheme)
     runner(args, origin, (ni, nj, gin.shape[2]))
     runner.ex.exchange([t_in2])
     np.save(os.path.join(outdir, f"out_{rank}.npy"), t_out.numpy())
@@ -177,12 +177,18 @@ def _global_inputs(periodic):
 
 
 @pytest.mark.parametrize(
-    "pi,pj,periodic,ifirst",
-    [(2, 2, (False, False), True), (3, 2, (False, False), True), (3, 2, (False, False), False),
-     (2, 2, (True, True), True), (2, 2, (True, True), False), (1, 2, (True, False), True), (2, 1, (False, True), True)],
+    "pi,pj,periodic,ifirst,scheme",
+    [(2, 2, (False, False), True, "two_phase"), (3, 2, (False, False), True, "two_phase"),
+     (3, 2, (False, False), False, "two_phase"), (2, 2, (True, True), True, "two_phase"),
+     (2, 2, (True, True), False, "two_phase"), (1, 2, (True, False), True, "two_phase"),
+     (2, 1, (False, True), True, "two_phase"),
+     (2, 2, (False, False), True, "diagonal"), (3, 2, (False, False), True, "diagonal"),
+     (2, 2, (True, True), True, "diagonal"), (1, 2, (True, False), True, "diagonal"),
+     (2, 1, (False, True), True, "diagonal"), (3, 3, (True, False), True, "diagonal")],
 )
-def test_2d_decomposition_matches_single_domain(tmp_path, pi, pj, periodic, ifirst):
-    """``ifirst``: I faces exchanged before a full-width interior (default) or west/east bands."""
+def test_2d_decomposition_matches_single_domain(tmp_path, pi, pj, periodic, ifirst, scheme):
+    """``scheme``: two exchange phases (``ifirst``: I faces before a full-width interior, else
+    west/east bands) or one phase with corner messages to the diagonal neighbours."""
     import torch.multiprocessing as mp
 
     sys.path.insert(0, REPO)
@@ -192,7 +198,7 @@ def test_2d_decomposition_matches_single_domain(tmp_path, pi, pj, periodic, ifir
 
     world = pi * pj
     port = _free_port()
-    mp.spawn(_worker2d, args=(world, port, str(tmp_path), pi, pj, periodic, ifirst), nprocs=world, join=True)
+    mp.spawn(_worker2d, args=(world, port, str(tmp_path), pi, pj, periodic, ifirst, scheme), nprocs=world, join=True)
     gin, gco = _global_inputs(periodic)
     h = 2
     nig, njg, nk = gco.shape

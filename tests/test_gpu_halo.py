@@ -70,7 +70,8 @@ def _oracle_hdiff(core, coeff, h, wrap_i):
     return out, padded
 
 
-@pytest.mark.parametrize("stream_mode", ["main", "main_bands", "side", "side_bands_main", "side_unpack_main", "side_split3"])
+@pytest.mark.parametrize("stream_mode", ["main", "main_bands", "side", "side_bands_main", "side_unpack_main", "side_split3",
+                                         "diag"])
 @pytest.mark.parametrize("mode", ["jstrips", "tiles2d", "tiles2d_jperiodic"])
 def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     import torch
@@ -88,12 +89,15 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     wrap_i = mode == "tiles2d"
     origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
     if mode == "jstrips":
+        if stream_mode == "diag":
+            pytest.skip("the diagonal (one-phase) scheme is a 2-D tile exchange")
         run = HaloStencil(st, ["in_field"], nj, h, 0, 1, periodic=True, force_comm=True)
         wrap_i = False
     else:
         dec = Decomposition2D(ni, nj, 1, 1, (wrap_i, True))
-        run = HaloStencil2D(st, ["in_field"], dec, 0, (h, h), force_comm=True)
-    run.stream_mode = stream_mode.split("_")[0]
+        run = HaloStencil2D(st, ["in_field"], dec, 0, (h, h), force_comm=True,
+                            scheme="diagonal" if stream_mode == "diag" else "two_phase")
+    run.stream_mode = {"diag": "main"}.get(stream_mode, stream_mode.split("_")[0])
     if hasattr(run, "bands_on_halo"):
         run.bands_on_halo = not stream_mode.endswith("bands_main")
         run.split = 3 if stream_mode.endswith("split3") else 1
