@@ -510,7 +510,14 @@ class PlaneGen:
                 B.append(f"if ({self.t_start + pp} >= {first} && {self.t_start + pp} < jce)")
                 B += ["    " + x for x in emit_load(v, self._row(f"({self.t_start + pp}) + ({v.lead})"),
                                                    [f"pf{pp}_{v.c}_{e}" for e in range(V)])]
-        B.append(f"for (int t = {self.t_start}; t < jce; ++t) {{")
+        # Option row_unroll=U (experiment): U copies of the row step per loop trip, each leaving
+        # the loop on its own (uniform) bound check, so the ring rotations between copies become
+        # register renames (U = lcm of the ring depths makes all of them renames).
+        row_unroll = int(self.opts.get("row_unroll", 0))
+        if row_unroll > 1:
+            B.append(f"for (int tt = {self.t_start}; ; tt += {row_unroll}) {{")
+        else:
+            B.append(f"for (int t = {self.t_start}; t < jce; ++t) {{")
         S = []
         for v in loads:
             first = -(v.needed_lo + v.lead)
@@ -538,7 +545,15 @@ class PlaneGen:
             for a in range(v.depth - 1, 0, -1):
                 for e in range(V):
                     S.append(f"{v.c}_{a}_{e} = {v.c}_{a - 1}_{e};")
-        B += ["    " + x for x in S]
+        if row_unroll > 1:
+            for u in range(row_unroll):
+                B.append(f"    {{  // row copy {u}")
+                B.append(f"        const int t = tt + {u};")
+                B.append("        if (t >= jce) break;")
+                B += ["        " + x for x in S]
+                B.append("    }")
+        else:
+            B += ["    " + x for x in S]
         B.append("}")
         return B
 

@@ -68,6 +68,8 @@ def test_jmirror_variants_build():
         src = open(os.path.join(os.path.dirname(_lib_path(ragged_chunk_stencil(opts))), "stencil.hip")).read()
         assert ("if ((chunk & 1) == 0) {" in src) == bool(opts["jmirror"])
         assert ("jb + jce - 1 - (" in src) == bool(opts["jmirror"])
+        u = opts.get("row_unroll", 0)
+        assert src.count("// row copy ") == (u * (2 if opts["jmirror"] else 1) * 2 if u > 1 else 0)
     # no J offsets (copy): nothing to mirror
     copy = gtscript.stencil(backend="gt:mi355x", definition=sc.copy_stencil, name="gpu.copy_mirror_check",
                             pointwise_plane=1)

@@ -173,7 +173,14 @@ def test_tridiag_full_size_vs_c_oracle():
         gu.assert_match(storage.to_numpy(devs[k]), ref[k], name=f"tridiag_full:{k}")
 
 
-RAGGED_CHUNK_OPTS = [{"jchunk": 4, "jmirror": 1}, {"jchunk": 8, "jmirror": 1}, {"jchunk": 8, "jmirror": 0}]
+RAGGED_CHUNK_OPTS = [
+    {"jchunk": 4, "jmirror": 1},
+    {"jchunk": 8, "jmirror": 1},
+    {"jchunk": 8, "jmirror": 0},
+    # row_unroll: U copies of the row step per trip, each leaving on its own bound check
+    {"jchunk": 8, "jmirror": 1, "row_unroll": 4},
+    {"jchunk": 4, "jmirror": 0, "row_unroll": 3},
+]
 
 
 def ragged_chunk_stencil(opts):
@@ -182,7 +189,7 @@ def ragged_chunk_stencil(opts):
     return gtscript.stencil(backend=BACKEND, definition=sc.hdiff_f64, name="gpu.hdiff_ragged", **opts)
 
 
-@pytest.mark.parametrize("opts", RAGGED_CHUNK_OPTS, ids=lambda o: f"jc{o['jchunk']}_m{o['jmirror']}")
+@pytest.mark.parametrize("opts", RAGGED_CHUNK_OPTS, ids=lambda o: f"jc{o['jchunk']}_m{o['jmirror']}_u{o.get('row_unroll', 0)}")
 @pytest.mark.parametrize("nj", [1, 3, 21, 22, 23, 37])
 def test_hdiff_ragged_j_chunks_vs_c_oracle(opts, nj):
     """Odd J chunks stream top-down (jmirror): last chunks of every length, both directions."""
