@@ -103,7 +103,7 @@ class Mi355xBackend(BaseBackend):
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
-        "row_unroll": {"versioning": True, "type": int, "description": "plane kernels: row steps per loop trip (ring rotations become renames; 0 = off, default)"},
+        "row_unroll": {"versioning": True, "type": int, "description": "plane kernels: row steps per loop trip (ring rotations become renames; 0 = off, -1 = auto: 4 for small register state, default)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

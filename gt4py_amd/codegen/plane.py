@@ -510,10 +510,16 @@ class PlaneGen:
                 B.append(f"if ({self.t_start + pp} >= {first} && {self.t_start + pp} < jce)")
                 B += ["    " + x for x in emit_load(v, self._row(f"({self.t_start + pp}) + ({v.lead})"),
                                                    [f"pf{pp}_{v.c}_{e}" for e in range(V)])]
-        # Option row_unroll=U (experiment): U copies of the row step per loop trip, each leaving
-        # the loop on its own (uniform) bound check, so the ring rotations between copies become
-        # register renames (U = lcm of the ring depths makes all of them renames).
-        row_unroll = int(self.opts.get("row_unroll", 0))
+        # row_unroll=U: U copies of the row step per loop trip, each leaving the loop on its own
+        # (uniform) bound check, so the ring rotations between copies become register renames.
+        # Auto (-1, default): 4 when the rings and prefetch buffers hold <= 40 32-bit words per
+        # lane (lap5: 32 words, +3 %; copy: neutral); kernels with more state lose occupancy
+        # (hdiff f64 80 words: -2.4 % at U=6; profiles/r02za_sweep_row_unroll*.log).
+        row_unroll = int(self.opts.get("row_unroll", -1))
+        if row_unroll < 0:
+            words = sum(v.depth * V * max(1, v.dtype.itemsize // 4) for v in self.vals if v.kind != "undef")
+            words += sum(P * V * max(1, v.dtype.itemsize // 4) for v in loads)
+            row_unroll = 4 if (V > 1 and words <= 40) else 0  # the 1-wide fallback stays rolled
         if row_unroll > 1:
             B.append(f"for (int tt = {self.t_start}; ; tt += {row_unroll}) {{")
         else:
