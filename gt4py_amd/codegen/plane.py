@@ -519,7 +519,14 @@ class PlaneGen:
         if row_unroll < 0:
             words = sum(v.depth * V * max(1, v.dtype.itemsize // 4) for v in self.vals if v.kind != "undef")
             words += sum(P * V * max(1, v.dtype.itemsize // 4) for v in loads)
-            row_unroll = 4 if (V > 1 and words <= 40) else 0  # the 1-wide fallback stays rolled
+            if V == 1:
+                row_unroll = 0  # the 1-wide fallback stays rolled
+            elif words <= 40:
+                row_unroll = 4
+            else:
+                # 4 cells per lane (f32): 2x (+0.7 %, +3.5 % on two boxes); 2 cells per lane
+                # (f64 hdiff): 2x/3x cost 3-4 % (profiles/r02za_sweep_row_unroll3.log)
+                row_unroll = 2 if V >= 4 else 0
         if row_unroll > 1:
             B.append(f"for (int tt = {self.t_start}; ; tt += {row_unroll}) {{")
         else:
