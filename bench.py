@@ -228,13 +228,20 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
             a[:, :, k] = rng.uniform(lo, hi, shape[:2])
         return a
 
+    second = None
     if sname == "horizontal_diffusion":
-        a = _demo_field(ni + 2 * h, nj + 2 * h, nk, dtype)
-        c = np.full((ni, nj, nk), 0.025, dtype=dtype, order="F")
+        # the GPU's field distributions (in U(-10,10), coeff U(0,0.5), bench Workload): the
+        # limiter branches are data-dependent, so the headline CPU figure uses the same mix
+        a = uni((ni + 2 * h, nj + 2 * h, nk), -10, 10)
+        c = uni((ni, nj, nk), 0.0, 0.5)
         o = np.zeros((ni, nj, nk), dtype=dtype, order="F")
         org = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
         fn = lambda: c_oracle.horizontal_diffusion(a, o, c, org, (ni, nj, nk), nthreads=threads)  # noqa: E731
-        inputs = "demo analytic in_field, coeff 0.025"
+        inputs = "in_field U(-10,10), coeff U(0,0.5), seed 1337 (the GPU's distributions)"
+        a_demo = _demo_field(ni + 2 * h, nj + 2 * h, nk, dtype)
+        c_demo = np.full((ni, nj, nk), 0.025, dtype=dtype, order="F")
+        second = ("demo analytic in_field, coeff 0.025",
+                  lambda: c_oracle.horizontal_diffusion(a_demo, o, c_demo, org, (ni, nj, nk), nthreads=threads))
     elif sname == "lap5":
         a = uni((ni + 2, nj + 2, nk), -10, 10)
         o = np.zeros((ni, nj, nk), order="F")
@@ -252,27 +259,42 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
         inputs = "U(-10,10) seed 1337"
     else:
         return {}
-    for _ in range(warm):
-        fn()
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        fn()
-        ts.append(time.perf_counter() - t0)
-    med = float(np.median(ts))
+
+    def median_s(f):
+        for _ in range(warm):
+            f()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    med = median_s(fn)
     cells = ni * nj * nk
-    return {
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    rec = {
         "value": round(cells / med / 1e6, 2),
         "unit": "Mcells/s",
         "cores": threads,
+        "affinity_cpus": affinity,
+        "os_cpu_count": os.cpu_count(),
         "kind": "port",
         "ms_per_call": round(med * 1e3, 3),
         "cpu_model": _cpu_model(),
         "sample": (f"cpu_ifirst-equivalent (own C++/OpenMP restatement, oracle/cpu_stencils.c) on the full "
                    f"{ni}x{nj}x{nk} {np.dtype(dtype).name} domain ({inputs}); median of {reps} calls after {warm} "
-                   f"warm-ups; {threads} threads, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
-                   f"OMP_PLACES={os.environ.get('OMP_PLACES')}"),
+                   f"warm-ups; {threads} OpenMP threads of the {affinity} CPUs in this process's affinity set, "
+                   f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, OMP_PLACES={os.environ.get('OMP_PLACES')}"),
     }
+    if second is not None:
+        med2 = median_s(second[1])
+        rec["second_input"] = {"inputs": second[0], "value": round(cells / med2 / 1e6, 2), "unit": "Mcells/s",
+                               "ms_per_call": round(med2 * 1e3, 3)}
+    return rec
 
 
 def cpu_baseline(cfg_name: str, reps: int = 20, warm: int = 3, timeout_s: float = 240.0):
@@ -612,11 +634,45 @@ def main():
 
     wl = Workload(args.config, args, rank, world, dev, backend, dry_run=args.dry_run)
     elapsed, kernel_ms = time_workload(wl, args.steps, args.warmup, dev, dist)
+    elapsed_rank = elapsed
     if dist is not None:
         tdev = dev if str(dist.get_backend()).lower() == "nccl" else "cpu"
         t = torch.tensor([elapsed, kernel_ms or 0.0], device=tdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), (float(t[1]) if kernel_ms is not None else None)
+    dist_rec = None
+    if dist is not None and world > 1:
+        # the same ranks, the same buffers: one plain launch over the whole local tile with no
+        # exchange, so the line says what the exchange costs per rank (max over ranks)
+        el_p, km_p = time_workload(wl, args.steps, args.warmup, dev, dist, step=wl.plain_step)
+        el_h2, _ = time_workload(wl, args.steps, args.warmup, dev, dist)  # halo path again, interleaved
+        el_hb = min(elapsed_rank, el_h2)
+        tdev = dev if str(dist.get_backend()).lower() == "nccl" else "cpu"
+        mine = torch.tensor([el_p, km_p or 0.0, el_hb / el_p - 1.0], device=tdev, dtype=torch.float64)
+        dist.all_reduce(mine, op=dist.ReduceOp.MAX)
+        ranks = [None] * world
+        me = {"rank": rank, "local_rank": local_rank, "host": os.uname().nodename}
+        if dev.type == "cuda":
+            p = torch.cuda.get_device_properties(dev)
+            me.update(device=torch.cuda.current_device(), pci_bus_id=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:"
+                      f"{p.pci_device_id:02x}.0", name=p.name)
+        dist.all_gather_object(ranks, me)
+        try:
+            rccl = ".".join(str(x) for x in torch.cuda.nccl.version()) if tdev is dev else None
+        except Exception:  # noqa: BLE001
+            rccl = None
+        dist_rec = {
+            "world_size": dist.get_world_size(),
+            "backend": str(dist.get_backend()),
+            "rccl_version": rccl,
+            "ranks": ranks,
+            "step_ms": round(kernel_ms, 4) if kernel_ms is not None else None,
+            "plain_ms_per_step": round(float(mine[0]) / args.steps * 1e3, 4),
+            "plain_kernel_ms": round(float(mine[1]), 4) if km_p is not None else None,
+            "exchange_overhead": round(float(mine[2]), 4),
+            "note": "plain = one launch over the whole local tile on the same buffers, no exchange; "
+                    "exchange_overhead = halo-path time / plain time - 1 per rank, max over ranks",
+        }
     halo_ab = None
     if args.halo_selfcomm and world == 1:
         # A/B on the same buffers in the same process: whole-domain launch without exchange,
@@ -633,7 +689,15 @@ def main():
     total_cells = wl.global_ij[0] * wl.global_ij[1] * nk * args.steps
     value = total_cells / elapsed / 1e6
     key = None if args.dry_run else wl.library_key()
-    traffic, traffic_src = (None, "dry run") if args.dry_run else traffic_for(args.config, key)
+    if wl.halo is not None:
+        # a halo step is interior + boundary strips + pack/unpack + RCCL: the single-launch pmc
+        # record of the stencil does not describe it
+        traffic, traffic_src = None, ("not measured for the halo step (interior + boundary strips + pack/unpack + "
+                                      "RCCL); profiles/pmc_<config>.json describes one plain launch")
+    elif args.dry_run:
+        traffic, traffic_src = None, "dry run"
+    else:
+        traffic, traffic_src = traffic_for(args.config, key)
     kms = kernel_ms if kernel_ms else elapsed / args.steps * 1e3
     achieved_gbs = cells_per_step * wl.bpc / (kms * 1e-3) / 1e9
     dec2d = wl.dec2d
@@ -674,11 +738,15 @@ def main():
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel_ms": round(kernel_ms, 4) if kernel_ms is not None else None,
+            # N=1: mean per-launch kernel time; with a halo path it is the HIP-event span of the
+            # whole step (exchange + interior + strips), so it is named step_ms there
+            ("kernel_ms" if wl.halo is None else "step_ms"): round(kernel_ms, 4) if kernel_ms is not None else None,
             "algorithmic_bytes_per_cell": wl.bpc,
             "library": key,
         },
     }
+    if dist_rec is not None:
+        result["dist"] = dist_rec
     if halo_ab is not None:
         result["halo_ab"] = halo_ab
     if world == 1 and not args.dry_run and not args.halo_selfcomm and args.sustain > 0:

@@ -78,6 +78,11 @@ class _Compiled:
             rows=rows,
         )
 
+    def bind(self, domain, origin, arrays, param_names):
+        """Prepared launch for the StencilObject fast path (``StencilLauncher.bind``)."""
+        return self.launcher.bind(domain, origin, arrays, param_names,
+                                  device_sync=bool(self.options.get("device_sync", True)))
+
 
 @register
 class Mi355xBackend(BaseBackend):
@@ -135,6 +140,7 @@ class Mi355xBackend(BaseBackend):
             compiled(domain, origin, exec_info, kwargs, rows)
 
         run_impl.compiled = compiled
+        run_impl.bind = compiled.bind  # fast path of repeated calls (stencil_object.py)
         run_impl.supports_rows = True  # gtmi_stencil_run_jsplit
         return run_impl
 

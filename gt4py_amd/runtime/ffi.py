@@ -100,6 +100,22 @@ def load_library(path: str) -> StencilLibrary:
         return _libs[path]
 
 
+def _to_bool(v) -> int:
+    return 1 if v else 0
+
+
+# dtype name -> (GtmiScalar member, Python conversion): the launcher's prepared scalar setters
+SCALAR_SLOTS = {
+    "float64": ("f64", float),
+    "float32": ("f32", float),
+    "int64": ("i64", int),
+    "int32": ("i32", int),
+    "int16": ("i16", int),
+    "int8": ("i8", int),
+    "bool": ("b", _to_bool),
+}
+
+
 def set_scalar(slot: GtmiScalar, dtype_name: str, value) -> None:
     if dtype_name == "float64":
         slot.f64 = float(value)

@@ -197,6 +197,59 @@ class StencilLauncher:
             f.dtype = ffi.DTYPE_IDS[np.dtype(dt).name]
         return fields, device, refs, ptrs
 
+    def bind(self, domain, origin, arrays: Dict[str, Any], param_names, *, device_sync=True):
+        """A prepared launch for repeated calls with these arrays, origins and domain: the fast
+        path of ``StencilObject.__call__`` / ``FrozenStencil.__call__`` (the caller checks that
+        the arrays are still the same objects with the same data pointers and shapes).
+
+        Returns ``launch(params) -> bool`` (``params``: the scalar values in ``param_names``
+        order; False when the call must take the ordinary path, e.g. another current device),
+        or None when this call cannot be prepared. Everything a call does not change -- the
+        packed ``gtmi_field`` array, the domain, the scalar slots, the foreign function -- is
+        built here once; a launch sets the scalars, reads torch's current raw stream and makes
+        the one foreign call.
+        """
+        import torch
+
+        lib = self.lib
+        fields, device = self.pack_fields(domain, origin, arrays)
+        if device is None or device.index is None:
+            return None
+        idx = device.index
+        n_sc = len(self.scalars)
+        scalars = (ffi.GtmiScalar * max(1, n_sc))()
+        setters = []
+        for j, s in enumerate(self.scalars):
+            if s["name"] in param_names:
+                attr, conv = ffi.SCALAR_SLOTS[s["dtype"]]
+                setters.append((scalars[j], param_names.index(s["name"]), attr, conv))
+            elif s.get("used", True):
+                return None
+            else:
+                ffi.set_scalar(scalars[j], s["dtype"], 0)
+        ni, nj, nk = (int(d) for d in domain)
+        dom = (ctypes.c_int64 * 3)(ni, nj, nk)
+        run = lib.run
+        n_fields = self.n_fields
+        raw_stream = torch._C._cuda_getCurrentRawStream
+        current_device = torch._C._cuda_getDevice
+        name = self.name
+
+        def launch(params) -> bool:
+            if current_device() != idx:
+                return False
+            for slot, pos, attr, conv in setters:
+                setattr(slot, attr, conv(params[pos]))
+            rc = run(dom, fields, n_fields, scalars, n_sc, raw_stream(idx))
+            if rc != 0:
+                raise RuntimeError(f"gt:mi355x stencil '{name}' failed: {lib.last_error()}")
+            if device_sync:
+                torch.cuda.current_stream(device).synchronize()
+            return True
+
+        launch.keep = (fields, scalars, dom)  # the foreign call borrows these
+        return launch
+
     def __call__(self, domain, origin, arrays: Dict[str, Any], params: Dict[str, Any], *, device_sync=True,
                  exec_info=None, rows=None) -> None:
         """``rows=(j_split, j_skip)``: only rows [0, j_split) and [j_split + j_skip, nj) of ``domain``

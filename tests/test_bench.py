@@ -35,6 +35,18 @@ def test_bench_launcher_dry_run(gpus, decomp):
     assert rec["config"]["global_domain"][1] == 32 * gpus
     if gpus > 1:
         assert rec["config"]["parallelism"].startswith("ij-")
+        # the N>1 line explains itself
+        d = rec["dist"]
+        assert d["world_size"] == gpus
+        assert [r["rank"] for r in d["ranks"]] == list(range(gpus))
+        assert "rccl_version" in d
+        for k in ("step_ms", "plain_ms_per_step", "plain_kernel_ms", "exchange_overhead"):
+            assert k in d
+        assert isinstance(d["exchange_overhead"], float)
+        assert rec["roofline"]["traffic"] is None and "halo step" in rec["roofline"]["traffic_source"]
+        assert "step_ms" in rec["roofline"] and "kernel_ms" not in rec["roofline"]
+    else:
+        assert "dist" not in rec
     for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "roofline", "config"):
         assert key in rec
 
