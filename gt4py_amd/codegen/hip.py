@@ -145,7 +145,7 @@ def generate(
     src = f"""// Generated by gt4py_amd (gt:mi355x). Do not edit.
 #include "gtmi_device.h"
 #include "gtmi.h"
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include "gtmi_roctx.h"
 #include <string.h>
 #include <stdio.h>
 
@@ -164,10 +164,10 @@ static int gtmi_run_rows(const int64_t* domain, int jsplit, int jskip, const gtm
     (void)sc; (void)f;
     const int ni = (int)domain[0], nj = (int)domain[1], nk = (int)domain[2];
     (void)ni; (void)nj; (void)nk; (void)jsplit; (void)jskip;
-    roctxRangePushA("{roctx_name}");  // ROCTX range around the launches (rocprofv3 --marker-trace)
+    GTMI_RANGE_PUSH("{roctx_name}");  // ROCTX range around the launches (rocprofv3 --marker-trace)
 {chr(10).join(host_scalars)}
 {chr(10).join("    " + line for h in launches for line in h.splitlines())}
-    roctxRangePop();
+    GTMI_RANGE_POP();
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {{
         snprintf(g_gtmi_err, sizeof(g_gtmi_err), "HIP launch failed: %s", hipGetErrorString(err));

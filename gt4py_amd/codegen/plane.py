@@ -446,8 +446,138 @@ class PlaneGen:
         geo = {"w_out": self.w_out, "V": V, "kname": kname, "used": used_slots}
         return "\n".join(L), geo
 
+    def _bufld_ok(self, V: int) -> bool:
+        """Row loads through buffer descriptors (option ``bufld``): 16- or 8-B lanes of 4/8-B types."""
+        if V < 2 or not int(self.opts.get("bufld", 0)) or not self.loads:
+            return False
+        stored = [n for n in self.current if self._mem_backed(n)]
+        if any(n in self.scratch for n in stored):
+            return False  # scratch stores cover the extent halo (edge-dependent conditions)
+        sizes = [v.dtype.itemsize for v in self.loads.values()] + [self.st.decl(n).dtype.itemsize for n in stored]
+        return all(x >= 4 and V * x in (8, 16) for x in sizes)
+
+    def _bufld_interior(self, V: int) -> str:
+        """Wave-uniform condition under which every lane that needs a loaded value finds its whole
+        vector inside the field's I range (all strips but the first and the last, typically)."""
+        conds = []
+        for v in self.loads.values():
+            lo, hi = self._lane_range(v)
+            c = cname(v.name)
+            conds.append(f"(w0 + {lo * V} >= p.ilo_{c}) && (w0 + {hi * V + V - 1} <= p.ihi_{c})")
+        # stores: the whole output strip inside the domain (every owned lane owns its whole vector:
+        # h_lo and w_out are multiples of V)
+        conds.append(f"(ib + {self.w_out} <= p.ni)")
+        return " && ".join(conds)
+
     def _render_body(self, V: int, P: int) -> List[str]:
-        """Register rings, prefetch and the row loop of one J direction."""
+        """Register rings, prefetch and the row loop of one J direction; with ``bufld`` the row
+        loop exists twice behind a wave-uniform branch: interior strips load every row through a
+        buffer descriptor (no branches around the loads), edge strips keep the clamped loads."""
+        if not self._bufld_ok(V):
+            return self._render_body_v(V, P)
+        B = [f"const bool bl_ok = __builtin_amdgcn_readfirstlane((int)({self._bufld_interior(V)})) != 0;",
+             "if (bl_ok) {"]
+        B += ["    " + x for x in self._render_body_slots(V, P)]
+        B.append("} else {")
+        B += ["    " + x for x in self._render_body_v(V, P)]
+        B.append("}")
+        return B
+
+    def _emit_bload(self, v: Val, row_expr: str, dests: List[str], rcond: str) -> List[str]:
+        """Unconditional row load: an invalid row gets a zero-record descriptor (no traffic), so
+        every row step issues the same loads and hipcc counts them exactly (vmcnt(N) instead of
+        vmcnt(0)), i.e. the prefetched rows really stay in flight."""
+        V = self.V
+        c = cname(v.name)
+        kexpr = f"kk + ({v.dk})" if v.dk else "kk"
+        nt = "true" if self._nt_load(v) else "false"
+        t = v.dtype.ctype
+        return [
+            "{",
+            f"    const int64_t ro = (int64_t)gtmi::clampi({row_expr}, p.jlo_{c}, p.jhi_{c}) * p.sJ_{c} + "
+            f"(int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c};",
+            f"    const __amdgpu_buffer_rsrc_t rs = gtmi::row_rsrc(p.p_{c} + ro + p.ilo_{c}, ({rcond}) ? nr_{v.c} : 0);",
+            f"    {t} tmp[{V}];",
+            f"    gtmi::bload<{t}, {V}, {nt}>(rs, bo_{v.c}, tmp);",
+        ] + [f"    {dests[e]} = tmp[{e}];" for e in range(V)] + ["}"]
+
+    def _render_body_slots(self, V: int, P: int) -> List[str]:
+        """Row loop of an interior strip with buffer-descriptor loads and slot rings.
+
+        Every loaded value (field, K offset) keeps the rows it still needs -- the J ring of the
+        section (``depth`` rows) plus the rows in flight (``P_v``) -- in ONE ring of ``U`` register
+        slots, ``U = max(depth) + P``, ``P_v = U - depth_v``; the loop is unrolled ``U`` times, so
+        copy ``u`` reads ring position ``a`` from slot ``(u - a) mod U`` and loads row
+        ``t + P_v`` into slot ``(u + P_v) mod U``, the slot its oldest row just left. No load
+        result is ever moved (a move of a row in flight would make hipcc wait for it), every
+        copy issues the same unconditional loads, and the waits count them exactly: each wave
+        keeps ``P_v`` rows of every stream in flight.
+        """
+        loads = list(self.loads.values())
+        U = max(v.depth for v in loads) + max(1, P)
+        B = []
+        for v in self.vals:  # rings of computed values (moves between VALU results only)
+            if v.kind in ("undef", "load"):
+                continue
+            for a in range(v.depth):
+                for e in range(V):
+                    B.append(f"{v.dtype.ctype} {v.c}_{a}_{e} = ({v.dtype.ctype})0;")
+        for v in loads:
+            lo, hi = self._lane_range(v)
+            c = cname(v.name)
+            # byte offset of the lane's vector from the row's first element; lanes that do not
+            # need the value point past the descriptor's range (the load returns 0, no traffic)
+            B.append(f"const int32_t bo_{v.c} = ((lane >= {lo}) && (lane <= {hi})) ? (pos - p.ilo_{c}) * "
+                     f"{v.dtype.itemsize} : (int32_t)0x40000000;")
+            B.append(f"const int32_t nr_{v.c} = (p.ihi_{c} - p.ilo_{c} + 1) * {v.dtype.itemsize};")
+            for k in range(U):
+                for e in range(V):
+                    B.append(f"{v.dtype.ctype} sl{k}_{v.c}_{e} = ({v.dtype.ctype})0;")
+        # prologue: rows t_start .. t_start + P_v - 1 into slots 0 .. P_v - 1
+        for v in loads:
+            first = -(v.needed_lo + v.lead)
+            pv = U - v.depth
+            for k in range(pv):
+                rcond = f"{self.t_start + k} >= {first} && {self.t_start + k} < jce"
+                B += self._emit_bload(v, self._row(f"({self.t_start + k}) + ({v.lead})"),
+                                      [f"sl{k}_{v.c}_{e}" for e in range(V)], rcond)
+        # the row loop must not inherit pending prologue loads: at the loop header hipcc merges
+        # the entry state with the back edge, and a prologue load still in flight there would
+        # pin the loop's waits to the prologue's registers
+        B.append("__builtin_amdgcn_s_waitcnt(0);  // prologue rows landed")
+        B.append(f"for (int tt = {self.t_start}; ; tt += {U}) {{")
+        for u in range(U):
+            S = []
+            for v in loads:
+                first = -(v.needed_lo + v.lead)
+                pv = U - v.depth
+                for a in range(v.depth):
+                    for e in range(V):
+                        S.append(f"const {v.dtype.ctype} {v.c}_{a}_{e} = sl{(u - a) % U}_{v.c}_{e};")
+                rcond = f"t + {pv} >= {first} && t + {pv} < jce"
+                S += self._emit_bload(v, self._row(f"t + {pv} + ({v.lead})"),
+                                      [f"sl{(u + pv) % U}_{v.c}_{e}" for e in range(V)], rcond)
+            for ti, code in enumerate(self.stage_code):
+                lead = self.stage_ext[ti][1][1]
+                S.append(f"{{  // stage {ti}: row t + {lead}")
+                S += ["    " + x for x in self._render_stage(ti, code, lead)]
+                S.append("}")
+            S += self._render_stores_buf()
+            for v in self.vals:
+                if v.kind in ("undef", "load"):
+                    continue
+                for a in range(v.depth - 1, 0, -1):
+                    for e in range(V):
+                        S.append(f"{v.c}_{a}_{e} = {v.c}_{a - 1}_{e};")
+            B.append(f"    {{  // row copy {u}")
+            B.append(f"        const int t = tt + {u};")
+            B.append("        if (t >= jce) break;")
+            B += ["        " + x for x in S]
+            B.append("    }")
+        B.append("}")
+        return B
+
+    def _render_body_v(self, V: int, P: int) -> List[str]:
         B = []
         # rings (+ per-element registers)
         for v in self.vals:
@@ -507,9 +637,11 @@ class PlaneGen:
         for v in loads:
             first = -(v.needed_lo + v.lead)
             for pp in range(P):
-                B.append(f"if ({self.t_start + pp} >= {first} && {self.t_start + pp} < jce)")
-                B += ["    " + x for x in emit_load(v, self._row(f"({self.t_start + pp}) + ({v.lead})"),
-                                                   [f"pf{pp}_{v.c}_{e}" for e in range(V)])]
+                rcond = f"{self.t_start + pp} >= {first} && {self.t_start + pp} < jce"
+                row = self._row(f"({self.t_start + pp}) + ({v.lead})")
+                dests = [f"pf{pp}_{v.c}_{e}" for e in range(V)]
+                B.append(f"if ({rcond})")
+                B += ["    " + x for x in emit_load(v, row, dests)]
         # row_unroll=U: U copies of the row step per loop trip, each leaving the loop on its own
         # (uniform) bound check, so the ring rotations between copies become register renames.
         # Auto (-1, default): 4 when the rings and prefetch buffers hold <= 40 32-bit words per
@@ -531,44 +663,74 @@ class PlaneGen:
             B.append(f"for (int tt = {self.t_start}; ; tt += {row_unroll}) {{")
         else:
             B.append(f"for (int t = {self.t_start}; t < jce; ++t) {{")
-        S = []
-        for v in loads:
-            first = -(v.needed_lo + v.lead)
-            if P == 0:
-                S.append(f"if (t >= {first})")
-                S += ["    " + x for x in emit_load(v, self._row(f"t + ({v.lead})"), [f"{v.c}_0_{e}" for e in range(V)])]
-            else:
+        def step_code(u: int) -> List[str]:
+            S = []
+            for v in loads:
+                first = -(v.needed_lo + v.lead)
+                if P == 0:
+                    S.append(f"if (t >= {first})")
+                    S += ["    " + x for x in emit_load(v, self._row(f"t + ({v.lead})"),
+                                                       [f"{v.c}_0_{e}" for e in range(V)])]
+                    continue
+                rcond = f"t + {P} >= {first} && t + {P} < jce"
+                row = self._row(f"t + {P} + ({v.lead})")
                 for e in range(V):
                     S.append(f"{v.c}_0_{e} = pf0_{v.c}_{e};")
                 for pp in range(P - 1):
                     for e in range(V):
                         S.append(f"pf{pp}_{v.c}_{e} = pf{pp + 1}_{v.c}_{e};")
-                S.append(f"if (t + {P} >= {first} && t + {P} < jce)")
-                S += ["    " + x for x in emit_load(v, self._row(f"t + {P} + ({v.lead})"),
-                                                   [f"pf{P - 1}_{v.c}_{e}" for e in range(V)])]
-        for ti, code in enumerate(self.stage_code):
-            lead = self.stage_ext[ti][1][1]
-            S.append(f"{{  // stage {ti}: row t + {lead}")
-            S += ["    " + x for x in self._render_stage(ti, code, lead)]
-            S.append("}")
-        S += self._render_stores()
-        for v in self.vals:
-            if v.kind == "undef":
-                continue
-            for a in range(v.depth - 1, 0, -1):
-                for e in range(V):
-                    S.append(f"{v.c}_{a}_{e} = {v.c}_{a - 1}_{e};")
+                dests = [f"pf{P - 1}_{v.c}_{e}" for e in range(V)]
+                S.append(f"if ({rcond})")
+                S += ["    " + x for x in emit_load(v, row, dests)]
+            for ti, code in enumerate(self.stage_code):
+                lead = self.stage_ext[ti][1][1]
+                S.append(f"{{  // stage {ti}: row t + {lead}")
+                S += ["    " + x for x in self._render_stage(ti, code, lead)]
+                S.append("}")
+            S += self._render_stores()
+            for v in self.vals:
+                if v.kind == "undef":
+                    continue
+                for a in range(v.depth - 1, 0, -1):
+                    for e in range(V):
+                        S.append(f"{v.c}_{a}_{e} = {v.c}_{a - 1}_{e};")
+            return S
+
         if row_unroll > 1:
             for u in range(row_unroll):
                 B.append(f"    {{  // row copy {u}")
                 B.append(f"        const int t = tt + {u};")
                 B.append("        if (t >= jce) break;")
-                B += ["        " + x for x in S]
+                B += ["        " + x for x in step_code(u)]
                 B.append("    }")
         else:
-            B += ["    " + x for x in S]
+            B += ["    " + x for x in step_code(0)]
         B.append("}")
         return B
+
+    def _render_stores_buf(self) -> List[str]:
+        """Stores of an interior strip: one unconditional buffer store per field and row; rows
+        outside the chunk get a zero-record descriptor, lanes outside the output strip an
+        offset past it (both dropped by the range check), so no branch surrounds a store."""
+        V = self.V
+        S = []
+        for name, v in self.current.items():
+            if not self._mem_backed(name):
+                continue
+            c = cname(name)
+            isz = self.st.decl(name).dtype.itemsize
+            t = v.dtype.ctype
+            row = self._row(f"t + ({v.lead})")
+            nts = "true" if self.opts.get("nt_store", 1) else "false"
+            S.append("{")
+            S.append(f"    const int64_t ro = (int64_t)({row}) * p.sJ_{c} + (int64_t)kk * p.sK_{c};")
+            S.append(f"    const bool rv = (t + ({v.lead}) >= 0) && (t + ({v.lead}) < jce);")
+            S.append(f"    const __amdgpu_buffer_rsrc_t rs = gtmi::row_rsrc(p.p_{c} + ro + p.ilo_{c}, "
+                     f"rv ? (p.ihi_{c} - p.ilo_{c} + 1) * {isz} : 0);")
+            S.append(f"    const {t} tmp[{V}] = {{{', '.join(f'{v.c}_0_{e}' for e in range(V))}}};")
+            S.append(f"    gtmi::bstore<{t}, {V}, {nts}>(rs, own_0 ? (pos - p.ilo_{c}) * {isz} : (int32_t)0x40000000, tmp);")
+            S.append("}")
+        return S
 
     def _render_stores(self) -> List[str]:
         V = self.V
@@ -682,7 +844,7 @@ class PlaneGen:
             H.append("            const long long nblocks = p.lvlsync  // per level: padded to a multiple of the 8 XCDs")
             H.append("                ? (long long)(((p.n_sgroups * p.n_chunks + 7) >> 3) * 8) * p.nks")
             H.append("                : (long long)p.n_sgroups * p.n_chunks * p.nks;")
-            H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); roctxRangePop(); return 2; }")
+            H.append("            if (nblocks > 0x7fffffffLL) { gtmi_set_error(\"grid too large\"); GTMI_RANGE_POP(); return 2; }")
             H.append("            p.perm_a = gtmi_coprime_multiplier((long long)nblocks);")
             H.append(
                 f"            hipLaunchKernelGGL({g['kname']}, dim3((unsigned)nblocks), "

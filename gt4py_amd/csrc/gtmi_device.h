@@ -200,6 +200,37 @@ template <typename T, int V, bool NT> GTMI_DEV void vstore(T* p, const T (&in)[V
     evec<T, V>* q = reinterpret_cast<evec<T, V>*>(p);
     if constexpr (NT) __builtin_nontemporal_store(x, q); else *q = x;
 }
+// Buffer descriptor of one row: `nbytes` valid bytes from `row` (0 = the row is skipped: every
+// load through it returns 0 without a memory access). Built from wave-uniform values only.
+GTMI_DEV __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), (short)0, nbytes, 0x00020000);
+}
+// V elements (8 or 16 bytes) at byte offset `off` of a row descriptor; NT = non-temporal
+template <typename T, int V, bool NT> GTMI_DEV void bload(__amdgpu_buffer_rsrc_t rs, int32_t off, T (&out)[V]) {
+    static_assert(sizeof(T) * V == 16 || sizeof(T) * V == 8, "bload moves 8 or 16 bytes");
+    if constexpr (sizeof(T) * V == 16) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, NT ? 2 : 0);
+        __builtin_memcpy(out, &x, 16);
+    } else {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, NT ? 2 : 0);
+        __builtin_memcpy(out, &x, 8);
+    }
+}
+// V elements (8 or 16 bytes) to byte offset `off` of a row descriptor (dropped when out of range)
+template <typename T, int V, bool NT> GTMI_DEV void bstore(__amdgpu_buffer_rsrc_t rs, int32_t off, const T (&in)[V]) {
+    static_assert(sizeof(T) * V == 16 || sizeof(T) * V == 8, "bstore moves 8 or 16 bytes");
+    if constexpr (sizeof(T) * V == 16) {
+        using W = decltype(__builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 0));
+        W x;
+        __builtin_memcpy(&x, in, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, NT ? 2 : 0);
+    } else {
+        using W = decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0));
+        W x;
+        __builtin_memcpy(&x, in, 8);
+        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, NT ? 2 : 0);
+    }
+}
 template <typename T, bool NT> GTMI_DEV T sload(const T* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p); else return *p;
 }

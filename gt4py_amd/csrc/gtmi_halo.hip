@@ -8,7 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include "gtmi_roctx.h"
 
 #include "gtmi_halo.h"
 
@@ -60,9 +60,9 @@ extern "C" int gtmi_halo_abi_version(void) { return GTMI_HALO_ABI_VERSION; }
 static int halo_copy_impl(const gtmi_box* boxes, int32_t n_boxes, int32_t direction, void* stream_ptr);
 
 extern "C" int gtmi_halo_copy(const gtmi_box* boxes, int32_t n_boxes, int32_t direction, void* stream_ptr) {
-    roctxRangePushA(direction == 0 ? "gtmi_halo:pack" : "gtmi_halo:unpack");
+    GTMI_RANGE_PUSH(direction == 0 ? "gtmi_halo:pack" : "gtmi_halo:unpack");
     const int rc = halo_copy_impl(boxes, n_boxes, direction, stream_ptr);
-    roctxRangePop();
+    GTMI_RANGE_POP();
     return rc;
 }
 

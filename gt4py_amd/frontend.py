@@ -1055,7 +1055,9 @@ class StencilParser:
                 )
         params: List[Any] = [self.fields[n] if n in self.fields else self.scalars[n] for n in self.api_order]
         return ir.Stencil(
-            name=func.__name__,
+            # the stencil's build name (gtscript.stencil(name=...), last component) as the
+            # reference's GTIR carries it, else the definition's
+            name=(getattr(self.options, "name", "") or func.__name__),
             api_signature=list(self.api_order),
             params=params,
             temporaries=list(self.temporaries.values()),

@@ -37,11 +37,15 @@ BASE_FLAGS = [
     "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wno-unused-variable",
     "-Wno-unused-but-set-variable",
-    # ROCTX ranges around every stencil call (rocprofv3 --marker-trace shows them by stencil name)
-    "-L/opt/rocm/lib",
-    "-lrocprofiler-sdk-roctx",
-    "-Wl,-rpath,/opt/rocm/lib",
 ]
+
+# ROCTX ranges around every stencil call (csrc/gtmi_roctx.h): only when this ROCm install has
+# rocprofiler-sdk-roctx; otherwise the ranges compile to nothing and nothing extra is linked
+_ROCTX_LIB = "/opt/rocm/lib/librocprofiler-sdk-roctx.so"
+if os.path.exists(_ROCTX_LIB) and os.environ.get("GTMI_BUILD_ROCTX", "1") != "0":
+    BASE_FLAGS += ["-DGTMI_ROCTX=1", "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
+else:
+    BASE_FLAGS += ["-DGTMI_ROCTX=0"]
 
 
 def hipcc_path() -> str:
@@ -60,7 +64,8 @@ def cache_root() -> str:
 
 def _headers_digest() -> str:
     h = hashlib.sha256()
-    for path in (os.path.join(CSRC_DIR, "gtmi_device.h"), os.path.join(INCLUDE_DIR, "gtmi.h")):
+    for path in (os.path.join(CSRC_DIR, "gtmi_device.h"), os.path.join(CSRC_DIR, "gtmi_roctx.h"),
+                 os.path.join(INCLUDE_DIR, "gtmi.h"), os.path.join(INCLUDE_DIR, "gtmi_halo.h")):
         with open(path, "rb") as f:
             h.update(f.read())
     return h.hexdigest()

@@ -161,6 +161,7 @@ class FrozenStencil:
         memo: Dict[tuple, tuple] = {}
         src = (
             "def _fast(kwargs):\n"
+            + f"    if len(kwargs) != {len(fnames) + len(pnames)}:\n        return False\n"
             + "".join(f"    {n} = kwargs.get({n!r})\n" for n in fnames + pnames)
             + f"    _gt_e = _memo.get({_ids_src(fnames)})\n"
             + f"    return _gt_e is not None and {_fast_check_src(fnames, 1)} and _gt_e[0]({_params_src(pnames)})\n"
@@ -171,10 +172,10 @@ class FrozenStencil:
         object.__setattr__(self, "_fast", ns["_fast"])
 
     def __call__(self, **kwargs) -> None:
+        if self._fast(kwargs):  # exactly the field and parameter arguments, a prepared launch
+            return
         assert "origin" not in kwargs and "domain" not in kwargs
         exec_info = kwargs.get("exec_info")
-        if exec_info is None and self._fast(kwargs):
-            return
         if exec_info is not None:
             exec_info["call_run_start_time"] = time.perf_counter()
         field_args = {name: kwargs[name] for name in self.stencil_object.field_info.keys()}

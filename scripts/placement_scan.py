@@ -35,6 +35,12 @@ def main():
     ap.add_argument("--scans", default="packed,out,gap,packed")
     ap.add_argument("--gaps-mib", default="0,1,2,4,6,8,16,32,64,128,256,512,1024")
     ap.add_argument("--config", default="hdiff")
+    ap.add_argument("--check", action="store_true",
+                    help="every variant's output must be bit-identical to the default library's (first placement)")
+    ap.add_argument("--probe-strides", default="",
+                    help="comma-separated byte strides: per placement, also time a strided sum over the triplet's "
+                         "bytes touching one element per stride (a TLB-reach probe: a few MB of traffic, one access "
+                         "per page at 4096)")
     ap.add_argument("--variants", default="",
                     help="';'-separated codegen option sets timed on every placement (e.g. 'order=5;order=3'); "
                          "the default library is always first")
@@ -97,6 +103,7 @@ def main():
         out = view(off_o, shp, str_o, (0, 0, 0))
         orig = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
         res = {}
+        ref = None
         for vn, st in stencils:
             call = lambda: st(fin, out, co, origin=orig, domain=shp, validate_args=False)  # noqa: E731
             call()
@@ -110,8 +117,39 @@ def main():
             torch.cuda.synchronize()
             ms = sorted(a.elapsed_time(b) for a, b in evs)
             res[vn] = round(ms[len(ms) // 2], 4)
+            if args.check and not checked:
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    same = bool(torch.equal(out, ref))
+                    print(json.dumps({"check": vn, "bit_identical": same}), flush=True)
+                    if not same:
+                        raise SystemExit(f"variant {vn} differs from the default library")
+                out.fill_(float("nan"))
+        if args.check:
+            checked.append(True)
         return res
 
+    probe_strides = [int(x) for x in args.probe_strides.split(",") if x]
+
+    def probe(off, nbytes):
+        """ms of a strided sum over [off, off + nbytes) of the pool, one element per stride."""
+        res = {}
+        for sb in probe_strides:
+            v = pool[off // it:(off + nbytes) // it:sb // it]
+            v.sum()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ts = []
+            for _ in range(5):
+                e0.record()
+                v.sum()
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            res[f"probe{sb}"] = round(sorted(ts)[2], 4)
+        return res
+
+    checked = []
     step = int(args.step_gb * (1 << 30))
     triple = bytes_in + 2 * bytes_o + 3 * 256
     for scan in args.scans.split(","):
@@ -119,11 +157,13 @@ def main():
             offs = range(0, pool_bytes - triple - 2 * MIB, step)
             for o in offs:
                 res = run(o, o + bytes_in + 256, o + bytes_in + bytes_o + 512)
+                res.update(probe(o, triple))
                 print(json.dumps({"scan": scan, "off_gb": round(o / (1 << 30), 2), "ms": res}), flush=True)
         elif scan == "out":
             lo = bytes_in + bytes_o + 512
             for o in range(lo, pool_bytes - bytes_o - 2 * MIB, step):
                 res = run(0, bytes_in + 256, o)
+                res.update(probe(o, bytes_o))
                 print(json.dumps({"scan": scan, "out_gb": round(o / (1 << 30), 2), "ms": res}), flush=True)
         elif scan == "gap":
             for g in (int(x) for x in args.gaps_mib.split(",")):

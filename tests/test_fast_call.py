@@ -1,0 +1,156 @@
+"""The cached-call fast path of ``StencilObject.__call__`` / ``FrozenStencil.__call__``
+(gt4py_amd/stencil_object.py, ``StencilLauncher.bind``): a repeated call with the same arrays,
+domain and origin skips argument extraction and packing. These tests pin that it never changes
+results: scalar parameters are re-read on every call, swapped / re-allocated / re-pointed
+(``set_``) / re-shaped arrays and changed domains or origins take the ordinary path, and
+``exec_info`` calls keep their timestamps. Every case is checked against numpy.
+"""
+
+import numpy as np
+import pytest
+
+from gt4py_amd import gtscript
+from gt4py_amd import storage as gt_storage
+from gt4py_amd.gtscript import PARALLEL, Field, computation, interval
+
+pytestmark = pytest.mark.gpu
+
+BK = "gt:mi355x"
+
+
+def _need_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def shift_axpy(a: Field[np.float64], b: Field[np.float64], *, w: np.float64):
+    with computation(PARALLEL), interval(...):
+        b = a[1, 0, 0] * w + a[0, 0, 0]
+
+
+def _expect(a, w, domain, org_a=(0, 0, 0), org_b=(0, 0, 0), b_init=None):
+    a = gt_storage.to_numpy(a)
+    ni, nj, nk = domain
+    out = np.array(b_init, copy=True)
+    ia, ja, ka = org_a
+    ib, jb, kb = org_b
+    out[ib:ib + ni, jb:jb + nj, kb:kb + nk] = (a[ia + 1:ia + 1 + ni, ja:ja + nj, ka:ka + nk] * w
+                                              + a[ia:ia + ni, ja:ja + nj, ka:ka + nk])
+    return out
+
+
+def _fields(seed, shape=(17, 9, 5)):
+    rng = np.random.default_rng(seed)
+    a = gt_storage.from_array(rng.uniform(-1, 1, (shape[0] + 1,) + shape[1:]), backend=BK, aligned_index=(0, 0, 0))
+    b = gt_storage.zeros(shape, np.float64, backend=BK)
+    return a, b
+
+
+def _memo(st):
+    return type(st)._gt_fast_memo_
+
+
+def test_repeated_calls_hit_and_reread_scalars():
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    a, b = _fields(1)
+    dom = (17, 9, 5)
+    for w in (0.5, 2.0, -3.25, 0.5):
+        st(a, b, w=w, domain=dom, origin=(0, 0, 0))
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a, w, dom, b_init=np.zeros(dom)))
+    assert len(_memo(st)) == 1
+
+
+def test_swapped_and_new_arrays():
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    dom = (16, 9, 5)
+    rng = np.random.default_rng(7)
+    x = gt_storage.from_array(rng.uniform(-1, 1, (17, 9, 5)), backend=BK, aligned_index=(0, 0, 0))
+    y = gt_storage.from_array(rng.uniform(-1, 1, (17, 9, 5)), backend=BK, aligned_index=(0, 0, 0))
+    for it in range(4):  # ping-pong: (x -> y), (y -> x), ... two memo entries
+        src, dst = (x, y) if it % 2 == 0 else (y, x)
+        want = _expect(src, 1.5, dom, b_init=gt_storage.to_numpy(dst))
+        st(src, dst, w=1.5, domain=dom, origin=(0, 0, 0))
+        np.testing.assert_array_equal(gt_storage.to_numpy(dst), want)
+    assert len(_memo(st)) == 2
+    for seed in range(3):  # fresh tensors every call (ids may be reused after a free)
+        a, b = _fields(100 + seed)
+        st(a, b, w=0.75, domain=(17, 9, 5), origin=(0, 0, 0))
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a, 0.75, (17, 9, 5), b_init=np.zeros((17, 9, 5))))
+        del a, b
+
+
+def test_set_and_resize_take_the_ordinary_path():
+    _need_gpu()
+    import torch
+
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    a, b = _fields(3)
+    dom = (17, 9, 5)
+    st(a, b, w=1.0, domain=dom, origin=(0, 0, 0))
+    a2, _ = _fields(4)
+    a.set_(a2.untyped_storage(), a2.storage_offset(), a2.shape, a2.stride())  # same object, new data
+    st(a, b, w=1.0, domain=dom, origin=(0, 0, 0))
+    np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a2, 1.0, dom, b_init=np.zeros(dom)))
+    # same object re-shaped in place (smaller): the cached validation must not be reused
+    b.resize_((4, 4, 4))
+    with pytest.raises(ValueError):
+        st(a, b, w=1.0, domain=dom, origin=(0, 0, 0))
+    torch.cuda.synchronize()
+
+
+def test_domain_and_origin_changes():
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    a, b = _fields(5)
+    full = (17, 9, 5)
+    st(a, b, w=2.0, domain=full, origin=(0, 0, 0))
+    b.zero_()
+    st(a, b, w=2.0, domain=(5, 4, 3), origin={"a": (1, 2, 1), "b": (3, 1, 2)})
+    np.testing.assert_array_equal(gt_storage.to_numpy(b),
+                                  _expect(a, 2.0, (5, 4, 3), (1, 2, 1), (3, 1, 2), b_init=np.zeros(full)))
+    b.zero_()
+    org = {"a": (1, 2, 1), "b": (3, 1, 2)}
+    st(a, b, w=2.0, domain=(5, 4, 3), origin=org)
+    org["b"] = (0, 0, 0)  # the caller mutates its origin dict: must not hit the stale entry
+    b.zero_()
+    st(a, b, w=2.0, domain=(5, 4, 3), origin=org)
+    np.testing.assert_array_equal(gt_storage.to_numpy(b),
+                                  _expect(a, 2.0, (5, 4, 3), (1, 2, 1), (0, 0, 0), b_init=np.zeros(full)))
+
+
+def test_exec_info_after_fast_calls():
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    a, b = _fields(6)
+    for _ in range(3):
+        st(a, b, w=1.0, domain=(17, 9, 5), origin=(0, 0, 0))
+    info = {}
+    st(a, b, w=1.0, domain=(17, 9, 5), origin=(0, 0, 0), exec_info=info)
+    for k in ("call_start_time", "call_end_time", "run_start_time", "run_end_time", "run_cpp_start_time"):
+        assert k in info
+
+
+def test_frozen_fast_path():
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    a, b = _fields(8)
+    dom = (17, 9, 5)
+    fz = st.freeze(origin={"a": (0, 0, 0), "b": (0, 0, 0)}, domain=dom)
+    for w in (1.0, -2.0, 0.125):
+        fz(a=a, b=b, w=w)
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a, w, dom, b_init=np.zeros(dom)))
+    assert len(fz._memo) == 1
+    a2, b2 = _fields(9)
+    fz(a=a2, b=b2, w=3.0)
+    np.testing.assert_array_equal(gt_storage.to_numpy(b2), _expect(a2, 3.0, dom, b_init=np.zeros(dom)))
+    info = {}
+    fz(a=a2, b=b2, w=3.0, exec_info=info)
+    assert "call_run_start_time" in info and "run_cpp_start_time" in info
