@@ -272,11 +272,14 @@ class HaloStencil:
                 self.exchange.finish(works)
                 self._strips(kw, origin, ni, nj, nk)
                 return
+            interior_done = main.record_event() if self.bands_on_halo else None
             with torch.cuda.stream(self._stream):
                 self.exchange.finish(works)
                 if self.bands_on_halo:
-                    # the two boundary strips follow the unpack on the halo stream: no stream
-                    # hand-off between the unpack and them (they write rows the interior does not)
+                    # the two boundary strips follow the unpack on the halo stream (they write rows
+                    # the interior does not) -- but only after the interior: both may use the
+                    # launcher's per-domain scratch buffers (a band as tall as the interior)
+                    self._stream.wait_event(interior_done)
                     self._strips(kw, origin, ni, nj, nk)
             main.wait_stream(self._stream)
             if self.bands_on_halo:

@@ -59,24 +59,28 @@ Box = Tuple[object, Tuple[int, int, int], Tuple[int, int, int], object]  # (fiel
 
 
 class BatchedCopy:
-    """Packs the ctypes descriptors of a fixed list of boxes once; ``run`` enqueues one launch."""
+    """Packs the ctypes descriptors of a fixed list of boxes once; ``run`` enqueues one launch per
+    ``MAX_BOXES`` boxes (one launch for every exchange phase up to 64 faces, i.e. 8 fields with the
+    diagonal scheme's 8 faces; more fields take further launches on the same stream)."""
 
     def __init__(self, boxes: Sequence[Box]):
-        if len(boxes) > MAX_BOXES:
-            raise ValueError(f"at most {MAX_BOXES} faces per batched halo copy")
         self.n = len(boxes)
-        self.arr = (GtmiBox * max(1, self.n))()
-        for b, (t, start, extent, buf) in zip(self.arr, boxes):
-            if t.dim() != 3 or not buf.is_contiguous() or buf.numel() < extent[0] * extent[1] * extent[2]:
-                raise ValueError("halo boxes need 3-D fields and large-enough contiguous buffers")
-            if buf.dtype != t.dtype:
-                raise TypeError("halo buffer dtype differs from the field's")
-            b.field = t.data_ptr()
-            b.strides[:] = t.stride()
-            b.start[:] = start
-            b.extent[:] = extent
-            b.buffer = buf.data_ptr()
-            b.itemsize = t.element_size()
+        self.parts = []
+        for c0 in range(0, self.n, MAX_BOXES):
+            chunk = boxes[c0:c0 + MAX_BOXES]
+            arr = (GtmiBox * len(chunk))()
+            for b, (t, start, extent, buf) in zip(arr, chunk):
+                if t.dim() != 3 or not buf.is_contiguous() or buf.numel() < extent[0] * extent[1] * extent[2]:
+                    raise ValueError("halo boxes need 3-D fields and large-enough contiguous buffers")
+                if buf.dtype != t.dtype:
+                    raise TypeError("halo buffer dtype differs from the field's")
+                b.field = t.data_ptr()
+                b.strides[:] = t.stride()
+                b.start[:] = start
+                b.extent[:] = extent
+                b.buffer = buf.data_ptr()
+                b.itemsize = t.element_size()
+            self.parts.append((arr, len(chunk)))
 
     def run(self, direction: int, stream=None) -> None:
         import torch
@@ -84,9 +88,10 @@ class BatchedCopy:
         if self.n == 0:
             return
         s = stream if stream is not None else torch.cuda.current_stream()
-        rc = _library().gtmi_halo_copy(self.arr, self.n, direction, ctypes.c_void_p(s.cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"gtmi_halo_copy failed: {_library().gtmi_halo_last_error().decode()}")
+        for arr, n in self.parts:
+            rc = _library().gtmi_halo_copy(arr, n, direction, ctypes.c_void_p(s.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"gtmi_halo_copy failed: {_library().gtmi_halo_last_error().decode()}")
 
 
 def slice_box(sl: Tuple[slice, slice], nk: int) -> Tuple[Tuple[int, int, int], Tuple[int, int, int]]:

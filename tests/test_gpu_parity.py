@@ -314,6 +314,31 @@ def test_stencil_graph_replay_matches_eager():
         assert np.array_equal(got, ref), trial
 
 
+def test_batched_halo_copy_more_than_64_faces():
+    """More faces than one launch carries (e.g. > 8 fields with the diagonal 2-D scheme): the
+    copy is split into launches of at most 64 faces, all on the same stream."""
+    torch = _torch()
+    from gt4py_amd.distributed.halo_copy import MAX_BOXES, BatchedCopy
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    fields = [torch.rand((19, 11, 3), generator=g, device=dev, dtype=torch.float64) for _ in range(9)]
+    boxes = []
+    for t in fields:  # 8 faces per field, as the diagonal scheme sends: 72 > 64
+        for q in range(8):
+            boxes.append((t, (q, q % 5, 0), (2 + q, 2, 3)))
+    assert len(boxes) > MAX_BOXES
+    bufs = [torch.empty(e[0] * e[1] * e[2], dtype=t.dtype, device=dev) for t, _, e in boxes]
+    bc = BatchedCopy([(t, s, e, buf) for (t, s, e), buf in zip(boxes, bufs)])
+    assert len(bc.parts) == 2
+    bc.run(0)
+    torch.cuda.synchronize()
+    for (t, s, e), buf in zip(boxes, bufs):
+        ref = t[s[0]:s[0] + e[0], s[1]:s[1] + e[1], s[2]:s[2] + e[2]].permute(2, 1, 0).reshape(-1)
+        assert torch.equal(buf, ref)
+
+
 def test_batched_halo_copy_roundtrip():
     """gtmi_halo_copy packs strided boxes of several fields into contiguous buffers and back."""
     torch = _torch()
