@@ -32,6 +32,7 @@ import time
 
 import numpy as np
 
+_START = time.time()
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -48,6 +49,10 @@ CONFIGS = {
     "vadv": ("vertical_advection_dycore", np.float64, (1024, 1024, 160), 0, 48),
     # hdiff written as three computations (lap / fluxes / update): fused into one launch
     "hdiff_blocks": ("horizontal_diffusion_blocks", np.float64, (2048, 2048, 160), 2, 24),
+    # a multi-stage stencil the two skeletons cannot take directly (a FORWARD recurrence feeding
+    # a temporary read at IJ offsets in a FORWARD loop): the staged lowering (SURVEY.md §8(f)
+    # row 1); algorithmic bytes: `a` read + `out` written
+    "staged": ("staged_forward_ij_temp", np.float64, (1024, 1024, 160), 1, 16),
     # shape probes for work-order experiments (scripts/sweep.py; never bench lines)
     "lap5_k160": ("lap5", np.float64, (1024, 1024, 160), 1, 16),
     "lap5_2k": ("lap5", np.float64, (2048, 2048, 80), 1, 16),
@@ -169,7 +174,19 @@ def stencil_defs():
                 flx[0, 0, 0] - flx[-1, 0, 0] + fly[0, 0, 0] - fly[0, -1, 0]
             )
 
+    def staged_forward_ij_temp(a: F64, out: F64):
+        # tests/stencil_cases.py staged_forward_ij_temp (golden-pinned)
+        with computation(FORWARD):
+            with interval(0, 1):
+                s = a
+            with interval(1, None):
+                s = s[0, 0, -1] * 0.5 + a
+        with computation(FORWARD), interval(...):
+            t = s * 2.0 + a
+            out = t[1, 0, 0] - t[-1, 0, 0] + t[0, 1, 0] * s
+
     return {
+        ("staged_forward_ij_temp", np.float64): staged_forward_ij_temp,
         ("horizontal_diffusion_blocks", np.float64): horizontal_diffusion_blocks,
         ("vertical_advection_dycore", np.float64): vertical_advection_dycore,
         ("horizontal_diffusion", np.float64): make_hdiff(np.float64),
@@ -318,6 +335,74 @@ def cpu_baseline(cfg_name: str, reps: int = 20, warm: int = 3, timeout_s: float 
 
 
 # ------------------------------------------------------------------------------------------
+# Box state (record which state a box is in). sysfs of the card this process uses:
+# identity, DPM clock levels, power and its cap, VRAM already in use before our allocations.
+# ------------------------------------------------------------------------------------------
+
+
+def _read_text(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def find_card(pci_bus_id: str):
+    """sysfs device directory of the GPU with this PCI bus id (``dddd:bb:dd.f``)."""
+    import glob
+
+    want = pci_bus_id.lower()
+    for d in sorted(glob.glob("/sys/class/drm/card*/device")):
+        for line in (_read_text(os.path.join(d, "uevent")) or "").splitlines():
+            if line.startswith("PCI_SLOT_NAME=") and line.split("=", 1)[1].lower() == want:
+                return d
+    return None
+
+
+def _dpm_current(text):
+    for line in (text or "").splitlines():
+        if line.rstrip().endswith("*"):
+            return line.split(":", 1)[-1].replace("*", "").strip()
+    return None
+
+
+def card_snapshot(card):
+    """Current DPM levels, power, temperatures and busy counters of the card (sysfs)."""
+    import glob
+
+    if card is None:
+        return {}
+    s = {clk: _dpm_current(_read_text(os.path.join(card, f"pp_dpm_{clk}"))) for clk in ("sclk", "mclk", "fclk", "socclk")}
+    s["gpu_busy"] = _read_text(os.path.join(card, "gpu_busy_percent"))
+    s["vram_used"] = _read_text(os.path.join(card, "mem_info_vram_used"))
+    hw = sorted(glob.glob(os.path.join(card, "hwmon", "hwmon*")))
+    if hw:
+        for name in ("power1_input", "power1_average", "power1_cap", "temp1_input", "temp2_input", "temp3_input"):
+            v = _read_text(os.path.join(hw[0], name))
+            if v is not None:
+                s[name] = v
+    return s
+
+
+def box_identity(dev_index: int = 0):
+    """(card sysfs dir, identity dict) of the device this process runs on."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev_index)
+    pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    card = find_card(pci)
+    ident = {"pci": pci, "name": p.name, "uuid": str(p.uuid), "cus": p.multi_processor_count}
+    if card is not None:
+        for name in ("product_name", "serial_number", "unique_id", "vbios_version"):
+            v = _read_text(os.path.join(card, name))
+            if v is not None:
+                ident[name] = v
+        ident["mclk_levels"] = (_read_text(os.path.join(card, "pp_dpm_mclk")) or "").replace("\n", "; ")
+    return card, ident
+
+
+# ------------------------------------------------------------------------------------------
 # Workloads
 # ------------------------------------------------------------------------------------------
 
@@ -407,6 +492,9 @@ class Workload:
             elif args.halo_selfcomm:
                 self.halo = HaloStencil(self.stencil, ["in_field"], nj, h, 0, 1, periodic=True, force_comm=True,
                                         overlap=overlap)
+        elif sname == "staged_forward_ij_temp":
+            self.args = (uniform((ni + 2 * h, nj + 2 * h, nk), -1, 1, (h, h, 0)), zeros((ni, nj, nk)))
+            self.origin = {"a": (h, h, 0), "out": (0, 0, 0)}
         elif sname == "tridiagonal_solver":
             self.args = tuple(uniform((ni, nj, nk), lo, hi) for lo, hi in ((-1, 1), (4, 5), (-1, 1), (-10, 10), (0, 0)))
             self.origin = (0, 0, 0)
@@ -484,6 +572,34 @@ def time_workload(wl, steps, warmup, dev, dist=None, events=True, step=None):
     return elapsed, kernel_ms
 
 
+def placement_probe(wl, n: int) -> dict:
+    """Kernel time of the workload's own launch when its output field lives in ``n`` other,
+    freshly allocated buffers (inputs unchanged): HIP-event median of 10 launches each."""
+    import torch
+
+    from gt4py_amd import storage
+
+    out0 = wl.named["out_field"]
+    ms = []
+    for _ in range(n):
+        alt = storage.zeros(tuple(out0.shape), wl.dtype, backend="gt:mi355x")
+        args = tuple(alt if a is out0 else a for a in wl.args)
+        call = lambda: wl.stencil(*args, **wl.params, origin=wl.origin, domain=wl.domain, validate_args=False)  # noqa: E731
+        call()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for a, b in evs:
+            a.record()
+            call()
+            b.record()
+        torch.cuda.synchronize()
+        t = sorted(a.elapsed_time(b) for a, b in evs)
+        ms.append(round(t[len(t) // 2], 4))
+        del alt, args
+        torch.cuda.empty_cache()
+    return {"out_field_buffers": n, "kernel_ms": ms, "min_ms": min(ms), "max_ms": max(ms),
+            "note": "same kernel and inputs, out_field in other HBM buffers; not part of the headline"}
+
+
 def traffic_for(cfg, key):
     """HBM bytes per launch from ``profiles/pmc_<cfg>.json`` -- only when that measurement was
     taken on the library this run executed (same build key); otherwise null plus the reason."""
@@ -500,7 +616,7 @@ def traffic_for(cfg, key):
     return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_{cfg}.json (library {key})"
 
 
-EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv", "hdiff_blocks")
+EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv", "hdiff_blocks", "staged")
 
 
 # ------------------------------------------------------------------------------------------
@@ -568,6 +684,8 @@ def main():
                     help="N=1: after the timed K steps, run the step for about this many seconds more and report "
                          "the steady-state ms/step as `sustained` (0 = off)")
     ap.add_argument("--jchunk", type=int, default=None)
+    ap.add_argument("--placement-probe", type=int, default=3,
+                    help="N=1: time the kernel with out_field in this many other fresh buffers (0 = off)")
     ap.add_argument("--opt", action="append", default=None, metavar="KEY=VALUE",
                     help="gt:mi355x codegen option for the headline config (repeatable)")
     ap.add_argument("--fill", default="bulk", choices=["slab", "bulk"],
@@ -632,6 +750,11 @@ def main():
 
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
 
+    box = None
+    if not args.dry_run:
+        card, ident = box_identity(torch.cuda.current_device())
+        box = {"identity": ident, "before": card_snapshot(card), "pid": os.getpid(),
+               "process_uptime_s": round(time.time() - _START, 2)}
     wl = Workload(args.config, args, rank, world, dev, backend, dry_run=args.dry_run)
     elapsed, kernel_ms = time_workload(wl, args.steps, args.warmup, dev, dist)
     elapsed_rank = elapsed
@@ -765,6 +888,20 @@ def main():
         result["full_call"] = {"validate_args": True, "sync_each_call": True,
                                "ms_per_call": round(el_v / args.steps * 1e3, 4),
                                "host_overhead_ms": round(el_v / args.steps * 1e3 - (kernel_ms or 0.0), 4)}
+    if world == 1 and not args.dry_run and not args.halo_selfcomm and args.placement_probe > 0 and wl.named:
+        # the same kernel on the same in/coeff buffers, writing into other freshly allocated
+        # out_field buffers: how much of the headline is the HBM placement of the output
+        # (DESIGN.md §5 "HBM placement"); the headline value stays the first allocation
+        result["placement_probe"] = placement_probe(wl, args.placement_probe)
+    if box is not None:
+        box["after"] = card_snapshot(find_card(box["identity"]["pci"]))
+        # the fields' virtual addresses modulo 2 MiB and 1 GiB (physical addresses are not visible
+        # from user space; hipMalloc blocks are 2 MiB aligned)
+        box["field_va_residues"] = {
+            k: {"mod_2MiB": t.data_ptr() % (2 << 20), "mod_1GiB": t.data_ptr() % (1 << 30)}
+            for k, t in (wl.named or {}).items()
+        }
+        result["box"] = box
     if args.dry_run:
         result["dry_run"] = True
         result["data"] = "synthetic; DRY RUN on CPU (numpy backend, gloo): not a measurement"

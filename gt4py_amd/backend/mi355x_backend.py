@@ -109,7 +109,7 @@ class Mi355xBackend(BaseBackend):
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
         "row_unroll": {"versioning": True, "type": int, "description": "plane kernels: row steps per loop trip (ring rotations become renames; 0 = off, -1 = auto: 4 for small register state, default)"},
-        "bufld": {"versioning": True, "type": int, "description": "plane kernels: interior strips load rows through buffer descriptors, branch-free, so prefetched rows stay in flight (1)"},
+        "bufld": {"versioning": True, "type": int, "description": "plane kernels: interior strips load rows through buffer descriptors, branch-free, so prefetched rows stay in flight (1 on, 0 off, -1 auto: on for 4-cell lanes, default)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

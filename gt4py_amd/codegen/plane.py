@@ -448,7 +448,13 @@ class PlaneGen:
 
     def _bufld_ok(self, V: int) -> bool:
         """Row loads through buffer descriptors (option ``bufld``): 16- or 8-B lanes of 4/8-B types."""
-        if V < 2 or not int(self.opts.get("bufld", 0)) or not self.loads:
+        mode = int(self.opts.get("bufld", -1))
+        if mode < 0:
+            # auto: 4-byte lanes (4 cells per lane). hdiff f32 8192x1024x160: +4..+11 % on every
+            # one of 24 HBM placements, bit-identical; hdiff f64 (2 cells per lane): -0.5 %
+            # (profiles/r03/r03c_bufld_ab_*.jsonl)
+            mode = 1 if V >= 4 else 0
+        if V < 2 or not mode or not self.loads:
             return False
         stored = [n for n in self.current if self._mem_backed(n)]
         if any(n in self.scratch for n in stored):
@@ -505,16 +511,24 @@ class PlaneGen:
         """Row loop of an interior strip with buffer-descriptor loads and slot rings.
 
         Every loaded value (field, K offset) keeps the rows it still needs -- the J ring of the
-        section (``depth`` rows) plus the rows in flight (``P_v``) -- in ONE ring of ``U`` register
-        slots, ``U = max(depth) + P``, ``P_v = U - depth_v``; the loop is unrolled ``U`` times, so
-        copy ``u`` reads ring position ``a`` from slot ``(u - a) mod U`` and loads row
-        ``t + P_v`` into slot ``(u + P_v) mod U``, the slot its oldest row just left. No load
+        section (``depth`` rows) plus the rows in flight (``P_v``) -- in ONE ring of ``R_v``
+        register slots (``R_v`` divides ``U = max(depth) + P``), ``P_v = R_v - depth_v``; the loop
+        is unrolled ``U`` times, so copy ``u`` reads ring position ``a`` from slot
+        ``(u - a) mod R_v`` and loads row ``t + P_v`` into slot ``(u + P_v) mod R_v``, the slot
+        its oldest row just left. No load
         result is ever moved (a move of a row in flight would make hipcc wait for it), every
         copy issues the same unconditional loads, and the waits count them exactly: each wave
         keeps ``P_v`` rows of every stream in flight.
         """
         loads = list(self.loads.values())
         U = max(v.depth for v in loads) + max(1, P)
+        # ring size per value: the smallest divisor of U that holds its J ring plus at least
+        # P - 1 rows in flight (U itself for the deepest ring): shallow streams (coeff) do not
+        # pay U - 1 rows of registers
+        ring: Dict[int, int] = {}
+        for v in loads:
+            need = v.depth + max(1, P - 1)
+            ring[v.vid] = U if v.depth + max(1, P) >= U else min(d for d in range(1, U + 1) if U % d == 0 and d >= need)
         B = []
         for v in self.vals:  # rings of computed values (moves between VALU results only)
             if v.kind in ("undef", "load"):
@@ -530,13 +544,13 @@ class PlaneGen:
             B.append(f"const int32_t bo_{v.c} = ((lane >= {lo}) && (lane <= {hi})) ? (pos - p.ilo_{c}) * "
                      f"{v.dtype.itemsize} : (int32_t)0x40000000;")
             B.append(f"const int32_t nr_{v.c} = (p.ihi_{c} - p.ilo_{c} + 1) * {v.dtype.itemsize};")
-            for k in range(U):
+            for k in range(ring[v.vid]):
                 for e in range(V):
                     B.append(f"{v.dtype.ctype} sl{k}_{v.c}_{e} = ({v.dtype.ctype})0;")
         # prologue: rows t_start .. t_start + P_v - 1 into slots 0 .. P_v - 1
         for v in loads:
             first = -(v.needed_lo + v.lead)
-            pv = U - v.depth
+            pv = ring[v.vid] - v.depth
             for k in range(pv):
                 rcond = f"{self.t_start + k} >= {first} && {self.t_start + k} < jce"
                 B += self._emit_bload(v, self._row(f"({self.t_start + k}) + ({v.lead})"),
@@ -550,13 +564,14 @@ class PlaneGen:
             S = []
             for v in loads:
                 first = -(v.needed_lo + v.lead)
-                pv = U - v.depth
+                R = ring[v.vid]
+                pv = R - v.depth
                 for a in range(v.depth):
                     for e in range(V):
-                        S.append(f"const {v.dtype.ctype} {v.c}_{a}_{e} = sl{(u - a) % U}_{v.c}_{e};")
+                        S.append(f"const {v.dtype.ctype} {v.c}_{a}_{e} = sl{(u - a) % R}_{v.c}_{e};")
                 rcond = f"t + {pv} >= {first} && t + {pv} < jce"
                 S += self._emit_bload(v, self._row(f"t + {pv} + ({v.lead})"),
-                                      [f"sl{(u + pv) % U}_{v.c}_{e}" for e in range(V)], rcond)
+                                      [f"sl{(u + pv) % R}_{v.c}_{e}" for e in range(V)], rcond)
             for ti, code in enumerate(self.stage_code):
                 lead = self.stage_ext[ti][1][1]
                 S.append(f"{{  // stage {ti}: row t + {lead}")

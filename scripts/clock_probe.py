@@ -10,7 +10,6 @@ runs that follow other GPU work (VERDICT r02 "next round" item 1).
     python3 scripts/clock_probe.py --seconds 60 --tag first > gpurun_out/probe_first.jsonl
 """
 import argparse
-import glob
 import json
 import os
 import sys
@@ -19,68 +18,6 @@ import types
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-
-
-def _read(path):
-    try:
-        with open(path) as f:
-            return f.read().strip()
-    except OSError:
-        return None
-
-
-def find_card(pci_bus_id: str):
-    """sysfs device directory of the GPU with this PCI bus id (``0000:xx:00.0``)."""
-    want = pci_bus_id.lower()
-    for d in sorted(glob.glob("/sys/class/drm/card*/device")):
-        ue = _read(os.path.join(d, "uevent")) or ""
-        for line in ue.splitlines():
-            if line.startswith("PCI_SLOT_NAME=") and line.split("=", 1)[1].lower().endswith(want[-7:]):
-                return d
-    return None
-
-
-def _cur_level(text):
-    if not text:
-        return None
-    for line in text.splitlines():
-        if line.rstrip().endswith("*"):
-            return line.split(":", 1)[-1].replace("*", "").strip()
-    return None
-
-
-def snapshot(card):
-    """Current DPM levels, power, temperature and busy counters of the card (sysfs)."""
-    if card is None:
-        return {}
-    s = {}
-    for clk in ("sclk", "mclk", "fclk", "socclk", "vclk", "dcefclk"):
-        s[clk] = _cur_level(_read(os.path.join(card, f"pp_dpm_{clk}")))
-    s["perf_level"] = _read(os.path.join(card, "power_dpm_force_performance_level"))
-    s["gpu_busy"] = _read(os.path.join(card, "gpu_busy_percent"))
-    s["mem_busy"] = _read(os.path.join(card, "mem_busy_percent"))
-    hw = sorted(glob.glob(os.path.join(card, "hwmon", "hwmon*")))
-    if hw:
-        h = hw[0]
-        for name in ("power1_average", "power1_input", "power1_cap", "power1_cap_max", "temp1_input",
-                     "temp2_input", "temp3_input", "freq1_input", "freq2_input"):
-            v = _read(os.path.join(h, name))
-            if v is not None:
-                s[name] = v
-    return s
-
-
-def static_info(card):
-    if card is None:
-        return {}
-    out = {}
-    for name in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "pp_dpm_socclk", "unique_id", "serial_number",
-                 "product_name", "current_link_speed", "current_link_width", "vbios_version",
-                 "mem_info_vram_used", "mem_info_vram_total", "pp_power_profile_mode"):
-        v = _read(os.path.join(card, name))
-        if v is not None:
-            out[name] = v
-    return out
 
 
 def main():
@@ -96,11 +33,9 @@ def main():
     import bench
 
     t_start = time.time()
-    props = torch.cuda.get_device_properties(0)
-    pci = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
-    card = find_card(pci)
-    head = {"tag": args.tag, "pci": pci, "card": card, "name": props.name, "uuid": str(props.uuid),
-            "static": static_info(card), "before": snapshot(card), "pid": os.getpid()}
+    card, ident = bench.box_identity(0)
+    snapshot = bench.card_snapshot
+    head = {"tag": args.tag, "card": card, "identity": ident, "before": snapshot(card), "pid": os.getpid()}
     print(json.dumps(head), flush=True)
     dev = torch.device("cuda", 0)
     ns = types.SimpleNamespace(decomp="jstrips", jchunk=None, opt=None, fill="bulk", no_overlap=False,

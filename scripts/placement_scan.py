@@ -41,6 +41,9 @@ def main():
                     help="comma-separated byte strides: per placement, also time a strided sum over the triplet's "
                          "bytes touching one element per stride (a TLB-reach probe: a few MB of traffic, one access "
                          "per page at 4096)")
+    ap.add_argument("--rw-probe", action="store_true",
+                    help="per placement, also time a plain write (fill_) over out's bytes and a plain read (sum) "
+                         "over in's bytes: does the placement effect follow the written or the read stream?")
     ap.add_argument("--variants", default="",
                     help="';'-separated codegen option sets timed on every placement (e.g. 'order=5;order=3'); "
                          "the default library is always first")
@@ -150,6 +153,25 @@ def main():
         return res
 
     checked = []
+    def rw_probe(off_in, off_o):
+        """GB/s of a plain read of in's bytes and a plain write of out's bytes (median of 5)."""
+        res = {}
+        for kind, off, nb in (("read", off_in, bytes_in), ("write", off_o, bytes_o)):
+            v = pool[off // it:(off + nb) // it]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ts = []
+            for _ in range(6):
+                e0.record()
+                if kind == "read":
+                    v.sum()
+                else:
+                    v.fill_(0.25)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            res[f"{kind}_GBs"] = round(nb / (sorted(ts[1:])[2] * 1e-3) / 1e9, 1)
+        return res
+
     step = int(args.step_gb * (1 << 30))
     triple = bytes_in + 2 * bytes_o + 3 * 256
     for scan in args.scans.split(","):
@@ -158,12 +180,16 @@ def main():
             for o in offs:
                 res = run(o, o + bytes_in + 256, o + bytes_in + bytes_o + 512)
                 res.update(probe(o, triple))
+                if args.rw_probe:
+                    res.update(rw_probe(o, o + bytes_in + bytes_o + 512))
                 print(json.dumps({"scan": scan, "off_gb": round(o / (1 << 30), 2), "ms": res}), flush=True)
         elif scan == "out":
             lo = bytes_in + bytes_o + 512
             for o in range(lo, pool_bytes - bytes_o - 2 * MIB, step):
                 res = run(0, bytes_in + 256, o)
                 res.update(probe(o, bytes_o))
+                if args.rw_probe:
+                    res.update(rw_probe(0, o))
                 print(json.dumps({"scan": scan, "out_gb": round(o / (1 << 30), 2), "ms": res}), flush=True)
         elif scan == "gap":
             for g in (int(x) for x in args.gaps_mib.split(",")):

@@ -210,6 +210,45 @@ def test_hdiff_ragged_j_chunks_vs_c_oracle(opts, nj):
     gu.assert_match(storage.to_numpy(out_d), ref, name=f"hdiff_ragged_nj{nj}")
 
 
+BUFLD_OPTS = [
+    {"bufld": 1, "jchunk": 8},
+    {"bufld": 1, "jchunk": 4, "jmirror": 0},
+    {"bufld": 1, "jchunk": 8, "prefetch": 3},
+    {"bufld": 1, "jchunk": 16, "prefetch": 1},
+]
+
+
+def bufld_stencil(dtype, opts):
+    from gt4py_amd import gtscript
+
+    defn = sc.hdiff_f64 if dtype == np.float64 else sc.hdiff_f32
+    return gtscript.stencil(backend=BACKEND, definition=defn, name="gpu.hdiff_bufld", **opts)
+
+
+@pytest.mark.parametrize("opts", BUFLD_OPTS, ids=lambda o: "_".join(f"{k}{v}" for k, v in o.items()))
+@pytest.mark.parametrize("dtype", [np.float64, np.float32], ids=["f64", "f32"])
+@pytest.mark.parametrize("ni,nj", [(150, 22), (1000, 37), (999, 1), (1111, 23)])
+def test_hdiff_bufld_strips_vs_c_oracle(opts, dtype, ni, nj):
+    """Plane kernels with buffer-descriptor row loads (bufld): interior strips take the branch-free
+    slot-ring loop, the first / last strip the clamped one; rows of every chunk length, both J
+    directions, several prefetch depths; cells outside the domain keep their sentinel."""
+    _torch()
+    from gt4py_amd import storage
+    from oracle import c_oracle
+
+    nk, h = 3, 2
+    stencil = bufld_stencil(dtype, opts)
+    rng = np.random.default_rng(ni + nj)
+    in_h, in_d = _alloc_fill((ni + 2 * h, nj + 2 * h, nk), dtype, rng, -10, 10, (h, h, 0))
+    co_h, co_d = _alloc_fill((ni, nj, nk), dtype, rng, 0, 0.5, (0, 0, 0))
+    out_d = storage.full((ni + 3, nj + 2, nk), -7.0, dtype, backend=BACKEND, aligned_index=(1, 1, 0))
+    org = {"in_field": (h, h, 0), "out_field": (1, 1, 0), "coeff": (0, 0, 0)}
+    stencil(in_d, out_d, co_d, origin=org, domain=(ni, nj, nk))
+    ref = np.full((ni + 3, nj + 2, nk), -7.0, dtype=dtype, order="F")
+    c_oracle.horizontal_diffusion(np.asfortranarray(in_h), ref, np.asfortranarray(co_h), org, (ni, nj, nk))
+    gu.assert_match(storage.to_numpy(out_d), ref, name=f"hdiff_bufld_{ni}x{nj}")
+
+
 def test_outside_domain_untouched():
     """Outputs are written inside the compute domain only (stencil_object.py contract)."""
     torch = _torch()
