@@ -289,10 +289,7 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
 
     med = median_s(fn)
     cells = ni * nj * nk
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
+    affinity = int(os.environ.get("GTMI_PARENT_AFFINITY", "0")) or None
     rec = {
         "value": round(cells / med / 1e6, 2),
         "unit": "Mcells/s",
@@ -304,7 +301,7 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
         "cpu_model": _cpu_model(),
         "sample": (f"cpu_ifirst-equivalent (own C++/OpenMP restatement, oracle/cpu_stencils.c) on the full "
                    f"{ni}x{nj}x{nk} {np.dtype(dtype).name} domain ({inputs}); median of {reps} calls after {warm} "
-                   f"warm-ups; {threads} OpenMP threads of the {affinity} CPUs in this process's affinity set, "
+                   f"warm-ups; {threads} OpenMP threads on the {affinity} CPUs of the bench process's affinity set, "
                    f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, OMP_PLACES={os.environ.get('OMP_PLACES')}"),
     }
     if second is not None:
@@ -319,7 +316,15 @@ def cpu_baseline(cfg_name: str, reps: int = 20, warm: int = 3, timeout_s: float 
     import subprocess
 
     env = dict(os.environ)
-    env.setdefault("OMP_NUM_THREADS", str(os.cpu_count() or 1))
+    # this (unbound) process's CPU set: the child's own affinity is a single core once libgomp has
+    # bound its master thread, and more threads than CPUs would only oversubscribe
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        ncpu = os.cpu_count() or 1
+    threads = min(int(env.get("OMP_NUM_THREADS") or ncpu), ncpu)
+    env["OMP_NUM_THREADS"] = str(threads)
+    env["GTMI_PARENT_AFFINITY"] = str(ncpu)
     env["OMP_PROC_BIND"] = "close"
     env["OMP_PLACES"] = "cores"
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", cfg_name, "--cpu-reps", str(reps),

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Does the hdiff time of a fresh process depend on what was allocated before its fields?
+
+One process = one allocation history: optionally hold ``--pre-gb`` GB of device memory, then
+build the bench workload (in_field, out_field, coeff through gt4py_amd.storage, in bench order)
+and time the kernel (HIP events, median of 20). Several processes in a row on one box compare
+histories; each prints one JSON line.
+
+    python3 scripts/alloc_probe.py --pre-gb 16 --tag pre16
+"""
+import argparse
+import json
+import os
+import sys
+import types
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="hdiff")
+    ap.add_argument("--pre-gb", type=float, default=0.0, help="device memory held before the fields")
+    ap.add_argument("--post-free", action="store_true", help="free the pre-allocation before timing")
+    ap.add_argument("--tag", default="")
+    args = ap.parse_args()
+
+    import torch
+
+    import bench
+
+    pre = None
+    if args.pre_gb > 0:
+        pre = torch.empty(int(args.pre_gb * (1 << 30)), dtype=torch.uint8, device="cuda")
+    ns = types.SimpleNamespace(decomp="jstrips", jchunk=None, opt=None, fill="bulk", no_overlap=False,
+                               halo_selfcomm=False)
+    wl = bench.Workload(args.config, ns, 0, 1, torch.device("cuda", 0), "gt:mi355x")
+    if pre is not None and args.post_free:
+        del pre
+        pre = None
+    torch.cuda.synchronize()
+    for _ in range(3):
+        wl.plain_step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+    for a, b in evs:
+        a.record()
+        wl.plain_step()
+        b.record()
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in evs)
+    rec = {"tag": args.tag, "pre_gb": args.pre_gb, "kernel_ms": round(ms[len(ms) // 2], 4),
+           "ptrs": {k: hex(t.data_ptr()) for k, t in (wl.named or {}).items()}}
+    rec["placement_probe"] = bench.placement_probe(wl, 2)["kernel_ms"]
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
