@@ -19,7 +19,7 @@ import time
 
 from gt4py_amd.backend.base import BaseBackend, register
 from gt4py_amd.codegen import hip as hipgen
-from gt4py_amd.codegen.lowering import fuse_parallel_loops, lower_data_dims, split_phases
+from gt4py_amd.codegen.lowering import fuse_parallel_loops, fuse_sequential_loops, lower_data_dims, split_phases
 from gt4py_amd.codegen.plan import UnsupportedStencil, make_plan
 from gt4py_amd.runtime import jit
 from gt4py_amd.runtime.launcher import StencilLauncher
@@ -45,6 +45,18 @@ def generate_source(analysis, opts):
         plan = make_plan(lowered, pointwise_plane=bool(opts.get("pointwise_plane", 1)))
         source, signature = hipgen.generate(lowered, plan, opts, abi_fields=abi, components=components)
     except UnsupportedStencil as direct_failure:
+        # tile kernels: sequential computations fused into one K sweep where legal, and a sweep
+        # that reads its own products across columns runs on overlapping 2-D tiles with an LDS
+        # plane per level (the reference's IJ caches, oir_optimizations/caches.py:44-90)
+        if int(opts.get("tile", 1)):
+            try:
+                seq = fuse_sequential_loops(lowered)
+                plan = make_plan(seq, pointwise_plane=bool(opts.get("pointwise_plane", 1)), tile=True)
+                if any(getattr(k, "tile", False) for k in plan.kernels):
+                    source, signature = hipgen.generate(seq, plan, opts, abi_fields=abi, components=components)
+                    return plan, source, signature
+            except UnsupportedStencil:
+                pass
         # staged fallback: split computations into phases, column kernels + scratch temporaries
         try:
             staged = split_phases(lowered)
@@ -110,6 +122,8 @@ class Mi355xBackend(BaseBackend):
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
         "row_unroll": {"versioning": True, "type": int, "description": "plane kernels: row steps per loop trip (ring rotations become renames; 0 = off, -1 = auto: 4 for small register state, default)"},
         "bufld": {"versioning": True, "type": int, "description": "plane kernels: interior strips load rows through buffer descriptors, branch-free, so prefetched rows stay in flight (1 on, 0 off, -1 auto: on for 4-cell lanes, default)"},
+        "tile": {"versioning": True, "type": int, "description": "sequential sweeps that read their own products across columns: tile kernels with LDS planes (1, default) instead of the staged lowering (0)"},
+        "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per 64-wide block (4, 8, 16)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

@@ -37,6 +37,7 @@ from gt4py_amd.codegen.common import (  # noqa: F401
 LDS_BYTES = 160 * 1024  # per CU (MI355X_MICROARCH.md); one 256-thread block may take all of it
 DEFAULT_RING = 8
 DEFAULT_KREG = 0  # register band levels (option ``kreg``)
+TILE_BY = 8  # tile mode: J rows of threads per block (64 x 8 = 512 threads, halo included)
 
 
 @dataclasses.dataclass
@@ -83,15 +84,27 @@ class ColumnGen:
         self.ext = (ilo, ihi, jlo, jhi)
         self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
         self.seg_tail = int(opts.get("seg_tail", 0)) == 1
+        self.tile = bool(getattr(kernel, "tile", False))
+        self.lds = set(getattr(kernel, "lds", ()))
+        if self.tile:
+            bx, by = self._block()
+            if bx - ilo - ihi < 8 or by - jlo - jhi < 1:
+                raise UnsupportedStencil(f"IJ extent {self.ext} too wide for a {bx}x{by} tile")
         self.info = {li: self._analyse_loop(li) for li in kernel.loops}
         self.kreg = 0
-        self.tail = self._plan_tail()
+        self.tail = None if self.tile else self._plan_tail()
 
     def _mem(self, name):
         return name in self.api or name in self.scratch
 
     def _block(self) -> Tuple[int, int]:
-        """Threads per block in I and J (option ``col_bx``: I width, 256 threads in total)."""
+        """Threads per block in I and J (option ``col_bx``: I width, 256 threads in total; tile
+        mode: 64 x ``tile_by`` threads, default 8, halo included)."""
+        if getattr(self.kernel, "tile", False):
+            by = int(self.opts.get("tile_by", TILE_BY))
+            if by not in (4, 8, 16):
+                raise ValueError(f"tile_by must be 4, 8 or 16, got {by}")
+            return 64, by
         bx = int(self.opts.get("col_bx", COLUMN_BLOCK[0]))
         if bx not in (64, 128, 256):
             raise ValueError(f"col_bx must be 64, 128 or 256, got {bx}")
@@ -110,6 +123,8 @@ class ColumnGen:
             conds.append(f"j >= {-c}")
         if d < jhi:
             conds.append(f"j < p.nj + {d}")
+        if self.tile:
+            conds.insert(0, "alive")
         return " && ".join(conds) if conds else None
 
     # ------------------------------------------------------------------ analysis
@@ -131,6 +146,8 @@ class ColumnGen:
                 if not isinstance(acc, ir.FieldAccess) or acc.name in direct:
                     continue
                 di, dj, dk = acc.offset
+                if acc.name in self.lds and (di or dj):
+                    continue  # tile mode: read from the level's LDS plane
                 rng = win.setdefault((acc.name, di, dj), [dk, dk])
                 rng[0], rng[1] = min(rng[0], dk), max(rng[1], dk)
                 if w:
@@ -289,7 +306,25 @@ class ColumnGen:
         L.append(f"__global__ void __launch_bounds__({bx * by}) k{k}_column(const K{k}Params p) {{")
         B = []
         eilo, eihi, ejlo, ejhi = self.ext
-        if int(self.opts.get("col_order", 1)) == 1:
+        if self.tile:
+            # overlapping tiles: block (ti, tj) owns output columns [ti*TI, ti*TI + TI) x
+            # [tj*TJ, tj*TJ + TJ) and its threads cover them plus the loop's IJ extent as halo;
+            # no thread returns early (every thread reaches every level's barrier)
+            TI, TJ = bx - eilo - eihi, by - ejlo - ejhi
+            B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
+            B.append("const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);")
+            B.append("const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;")
+            B.append("const int w = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;")
+            B.append("const int tx = (int)threadIdx.x, ty = (int)threadIdx.y;")
+            B.append(f"const int i = (w % nbx) * {TI} + tx - {eilo};")
+            B.append(f"const int j = (w / nbx) * {TJ} + ty - {ejlo};")
+            B.append(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};")
+            B.append(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && ty < {ejlo + TJ} && "
+                     f"i < p.ni && j < p.nj;")
+            for n in sorted(self.lds):
+                ct = self.st.decl(n).dtype.ctype
+                B.append(f"__shared__ {ct} lds_{cname(n)}[2][{by}][{bx}];  // this level's plane (k & 1)")
+        elif int(self.opts.get("col_order", 1)) == 1:
             # XCD-aware: consecutive column blocks (along I, then J) run on one XCD (8 XCDs, round-robin dispatch)
             B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
             B.append("const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);")
@@ -300,7 +335,8 @@ class ColumnGen:
         else:
             B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x) - {eilo};")
             B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y) - {ejlo};")
-        B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
+        if not self.tile:
+            B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
         B.append("const int nk = p.nk;")
         for s in scalars:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
@@ -365,10 +401,17 @@ class ColumnGen:
             H.append("        }")
         else:
             H.append("        p.tail_len = 0;")
-        H.append(
-            f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
-            f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
-        )
+        if self.tile:
+            TI, TJ = bx - eilo - eihi, by - ejlo - ejhi
+            H.append(
+                f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {TI - 1}) / {TI}), "
+                f"(unsigned)((nj + {TJ - 1}) / {TJ})), dim3({bx}, {by}), {lds}, stream, p);"
+            )
+        else:
+            H.append(
+                f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
+                f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
+            )
         H.append("    }")
         H.append("}")
         return "\n".join(L), "\n".join(H)
@@ -515,6 +558,8 @@ class ColumnGen:
                 di, dj, dk = acc.offset
                 if acc.name in direct:
                     return mem_index(acc.name, di, dj, kaddr(acc))
+                if acc.name in self.lds and (di or dj):
+                    return f"lds_{cname(acc.name)}[k & 1][ty + ({dj})][tx + ({di})]"
                 return wvar(acc.name, di, dj, dk)
 
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
@@ -561,12 +606,26 @@ class ColumnGen:
 
             def statements() -> List[str]:
                 body = [f"k_next = k {step} 1;"]
+                pending: Set[str] = set()  # LDS planes written since the last barrier (tile mode)
                 for ti, s in enumerate(sec.body):
+                    if self.lds:
+                        reads = {a.name for a, w in iter_accesses([s])
+                                 if not w and isinstance(a, ir.FieldAccess) and a.name in self.lds
+                                 and (a.offset[0] or a.offset[1])}
+                        if reads & pending:
+                            body.append("gtmi::lds_barrier();  // the level's planes are complete")
+                            pending.clear()
                     code = self._stmt(s, rend, wvar, mem_store)
                     g = self._guard(li, si, ti)
                     if g:
                         code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
                     body += code
+                    if self.lds:
+                        pending |= {a.name for a, w in iter_accesses([s]) if w and a.name in self.lds}
+                if pending:
+                    # planes written but not read across columns at this level: the next write of
+                    # the same buffer (two levels on) must not overtake a slow reader
+                    body.append("gtmi::lds_barrier();")
                 if tail_write and band_now[0] == "reg":
                     body.append("// register band: this level's final values")
                     body += [f"rb_{cname(n)}_{reg_now[0]} = {wvar(n, 0, 0, 0)};" for n in tail_write]
@@ -730,14 +789,20 @@ class ColumnGen:
             name = s.target.name
             if name in self.direct:
                 st = mem_store(name, self._kaddr(s.target), rend(s.value))
-                if name in self.api and any(self.ext):
+                if name in self.api and self.tile:
+                    st = f"if (own) {st}"
+                elif name in self.api and any(self.ext):
                     st = f"if (i >= 0 && i < p.ni && j >= 0 && j < p.nj) {st}"
                 return [st]
             tgt = wvar(name, 0, 0, 0)
             out = [f"{tgt} = {rend(s.value)};"]
+            if name in self.lds:
+                out.append(f"lds_{cname(name)}[k & 1][ty][tx] = {tgt};")
             if self._mem(name):
                 st = mem_store(name, "k", tgt)
-                if name in self.api and any(self.ext):
+                if name in self.api and self.tile:
+                    st = f"if (own) {st}"  # overlapping tiles: each output column has one owner
+                elif name in self.api and any(self.ext):
                     st = f"if (i >= 0 && i < p.ni && j >= 0 && j < p.nj) {st}"
                 out.append(st)
             return out

@@ -306,3 +306,110 @@ def fuse_parallel_loops(analysis: StencilAnalysis) -> StencilAnalysis:
         passes.compute_k_boundary(new),
         analysis.min_k_size,
     )
+
+
+# ------------------------------------------------------------------------------------------
+# fusion of consecutive sequential computations (for the tile kernel)
+# ------------------------------------------------------------------------------------------
+
+
+def _whole_range(vl: ir.VerticalLoop) -> bool:
+    if len(vl.sections) != 1:
+        return False
+    itv = vl.sections[0].interval
+    return (itv.start.level == ir.LevelMarker.START and itv.start.offset == 0
+            and itv.end.level == ir.LevelMarker.END and itv.end.offset == 0)
+
+
+def _covers_range(vl: ir.VerticalLoop) -> bool:
+    """Sections contiguous from START+0 to END+0 (taken in level order: a BACKWARD
+    computation usually lists its top interval first)."""
+    rank = {ir.LevelMarker.START: 0, ir.LevelMarker.END: 1}
+    secs = sorted(vl.sections, key=lambda s: (rank[s.interval.start.level], s.interval.start.offset))
+    if not secs:
+        return False
+    s0, s1 = secs[0].interval.start, secs[-1].interval.end
+    if not (s0.level == ir.LevelMarker.START and s0.offset == 0 and s1.level == ir.LevelMarker.END and s1.offset == 0):
+        return False
+    for a, b in zip(secs, secs[1:]):
+        if a.interval.end.level != b.interval.start.level or a.interval.end.offset != b.interval.start.offset:
+            return False
+    return True
+
+
+def _aligned_sections(a: ir.VerticalLoop, b: ir.VerticalLoop):
+    """Pairs of (interval, body_a, body_b) over a common partition of the levels, or None."""
+    if _same_intervals(a, b):
+        return [(sa.interval, sa.body, sb.body, sa.def_index) for sa, sb in zip(a.sections, b.sections)]
+    if _whole_range(b) and _covers_range(a):
+        return [(sa.interval, sa.body, b.sections[0].body, sa.def_index) for sa in a.sections]
+    if _whole_range(a) and _covers_range(b):
+        return [(sb.interval, a.sections[0].body, sb.body, sb.def_index) for sb in b.sections]
+    return None
+
+
+def _seq_fusable(a: ir.VerticalLoop, b: ir.VerticalLoop, api: set) -> bool:
+    """Can sequential computation ``b`` run inside ``a``'s K sweep (statements appended per
+    level) without changing any result? Same order (FORWARD or BACKWARD), aligned intervals, no
+    run-time K offsets, no name written by both, ``a`` reads nothing ``b`` writes, and every
+    read in ``b`` of a value ``a`` produces is at a level the fused sweep has already produced
+    (K offset <= 0 forward, >= 0 backward), at the same level when it is read across columns
+    (the tile kernel exchanges one level through LDS), never an API field across columns."""
+    if a.loop_order != b.loop_order or a.loop_order == ir.LoopOrder.PARALLEL:
+        return False
+    if _aligned_sections(a, b) is None:
+        return False
+    fwd = a.loop_order == ir.LoopOrder.FORWARD
+    acc_a = [x for sec in a.sections for x in passes.iter_accesses(sec.body)]
+    acc_b = [x for sec in b.sections for x in passes.iter_accesses(sec.body)]
+    for acc, _ in acc_a + acc_b:
+        if isinstance(acc, ir.FieldAccess) and acc.k_offset is not None:
+            return False
+    wa = {acc.name for acc, w in acc_a if w}
+    wb = {acc.name for acc, w in acc_b if w}
+    if wa & wb:
+        return False
+    for acc, w in acc_a:
+        if not w and acc.name in wb:
+            return False
+    for acc, w in acc_b:
+        if w or not isinstance(acc, ir.FieldAccess) or acc.name not in wa:
+            continue
+        di, dj, dk = acc.offset
+        if (dk > 0) if fwd else (dk < 0):
+            return False
+        if (di or dj) and (dk != 0 or acc.name in api):
+            return False
+    return True
+
+
+def fuse_sequential_loops(analysis: StencilAnalysis) -> StencilAnalysis:
+    """Merge consecutive FORWARD (or BACKWARD) computations into one K sweep when legal
+    (``_seq_fusable``), so that a column recurrence feeding a temporary that a later computation
+    reads across columns (``staged_forward_ij_temp``) needs neither a scratch field for the
+    recurrence nor a second sweep: the tile kernel (``codegen/column.py``, tile mode) then runs
+    the whole sweep with the cross-column temporary in an LDS plane per level. Used only when the
+    two skeletons cannot take the computations as written; per column and level the statements
+    run in the original order, so no result changes."""
+    st = analysis.stencil
+    api = {p.name for p in st.field_params()}
+    loops: List[ir.VerticalLoop] = []
+    for vl in st.vertical_loops:
+        if loops and _seq_fusable(loops[-1], vl, api):
+            prev = loops[-1]
+            loops[-1] = ir.VerticalLoop(
+                prev.loop_order,
+                [ir.Section(itv, list(ba) + list(bb), di) for itv, ba, bb, di in _aligned_sections(prev, vl)],
+            )
+        else:
+            loops.append(vl)
+    if len(loops) == len(st.vertical_loops):
+        return analysis
+    new = dataclasses.replace(st, vertical_loops=loops)
+    return StencilAnalysis(
+        new,
+        passes.compute_access_kinds(new),
+        passes.compute_extents(new),
+        passes.compute_k_boundary(new),
+        analysis.min_k_size,
+    )

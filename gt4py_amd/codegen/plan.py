@@ -44,6 +44,11 @@ class PlaneKernel:
 @dataclasses.dataclass
 class ColumnKernel:
     loops: List[int]
+    # tile mode (one sequential loop): blocks own overlapping 2-D tiles of columns with the loop's
+    # IJ extent as halo, and the values in ``lds`` -- produced in the loop and read at IJ offsets
+    # at the same level -- are exchanged through an LDS plane per level (codegen/column.py)
+    tile: bool = False
+    lds: Tuple[str, ...] = ()
 
     def items(self, stencil):
         return [(li, si) for li in self.loops for si in range(len(stencil.vertical_loops[li].sections))]
@@ -92,10 +97,28 @@ def sections_contiguous(vl: ir.VerticalLoop) -> bool:
     return True
 
 
-def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_plane: bool = False) -> KernelPlan:
+def _tile_lds_names(vl: ir.VerticalLoop) -> Optional[List[str]]:
+    """Names a sequential loop produces and reads at IJ offsets, if a tile kernel can take the
+    loop (every such read at K offset 0, no run-time K offsets on them); None otherwise."""
+    written = {acc.name for acc, w in _loop_accesses(vl) if w}
+    names: List[str] = []
+    for acc, w in _loop_accesses(vl):
+        if w or not isinstance(acc, ir.FieldAccess) or acc.name not in written:
+            continue
+        if acc.offset[0] or acc.offset[1]:
+            if acc.offset[2] != 0 or acc.k_offset is not None:
+                return None
+            if acc.name not in names:
+                names.append(acc.name)
+    return names
+
+
+def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_plane: bool = False,
+              tile: bool = False) -> KernelPlan:
     """``column_only``: every computation runs in column kernels (the staged fallback, after
     ``lowering.split_phases``); otherwise PARALLEL computations with horizontal offsets become
-    J-streaming plane kernels."""
+    J-streaming plane kernels. ``tile``: a sequential computation that reads its own products at
+    IJ offsets (same level) becomes a tile-mode column kernel instead of being rejected."""
     st = analysis.stencil
     temps = {t.name for t in st.temporaries}
     api = {p.name for p in st.field_params()}
@@ -123,6 +146,12 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_pl
             for si in range(len(vl.sections)):
                 kernels.append(PlaneKernel(li, si))
         else:
+            lds = _tile_lds_names(vl) if (tile and vl.loop_order != ir.LoopOrder.PARALLEL) else None
+            if lds:
+                # a tile kernel of its own: its products cross columns through LDS, every level
+                flush()
+                kernels.append(ColumnKernel([li], tile=True, lds=tuple(lds)))
+                continue
             if vl.loop_order != ir.LoopOrder.PARALLEL:
                 # sequential loops: values produced in the loop may not be read at IJ offsets
                 written = set()
@@ -205,7 +234,7 @@ def make_plan(analysis: StencilAnalysis, column_only: bool = False, pointwise_pl
             scratch.append(t.name)
     # column kernels must not read scratch temporaries written inside the same kernel at IJ offsets
     for k in kernels:
-        if isinstance(k, ColumnKernel):
+        if isinstance(k, ColumnKernel) and not k.tile:
             written = set()
             for li in k.loops:
                 for acc, w in _loop_accesses(st.vertical_loops[li]):

@@ -238,3 +238,10 @@ template <typename T, bool NT> GTMI_DEV void sstore(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
 }
 }  // namespace gtmi
+
+namespace gtmi {
+// Workgroup barrier for LDS exchange only: waits for this wave's LDS operations, then s_barrier.
+// Loads and stores to global memory stay in flight across it (__syncthreads() would also drain
+// them with vmcnt(0)); the "memory" clobber keeps the compiler from moving LDS accesses across.
+GTMI_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+}  // namespace gtmi
