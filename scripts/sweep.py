@@ -105,6 +105,12 @@ def main():
         check = [ust for _ in variants]
         params = {"dtr_stage": 3.0 / 20.0}
         origin = (0, 0, 0)
+    elif sname == "staged_forward_ij_temp":
+        a = uniform((ni + 2 * h, nj + 2 * h, nk), -1, 1, (h, h, 0))
+        shared = storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x")
+        argsets = [(a, shared) for _ in variants]
+        check = [shared for _ in variants]
+        origin = {"a": (h, h, 0), "out": (0, 0, 0)}
     else:
         a = uniform((ni, nj, nk), -10, 10, (0, 0, 0))
         shared = storage.zeros((ni, nj, nk), dtype, backend="gt:mi355x")

@@ -93,7 +93,7 @@ CASES = {
     "fwd_recurrence_ij_temp": (fwd_recurrence_ij_temp, {"a": (1, 1, 0, 1)}, np.float64),
     "bwd_recurrence_ij_temp": (bwd_recurrence_ij_temp, {"a": (2, 2, 1, 1), "b": (2, 2, 1, 1)}, np.float64),
     "two_phase_chain": (two_phase_chain, {"a": (1, 1, 1, 1), "c": (1, 1, 1, 1)}, np.float64),
-    "tile_with_k_window": (tile_with_k_window, {"a": (1, 0, 1, 0), "w": (1, 0, 1, 0)}, np.float64),
+    "tile_with_k_window": (tile_with_k_window, {"a": (0, 1, 1, 0), "w": (0, 1, 1, 0)}, np.float64),
     "tile_conditional": (tile_conditional, {"a": (1, 1, 1, 1)}, np.float64),
     "tile_f32": (tile_f32, {"a": (1, 1, 1, 1)}, np.float32),
 }
@@ -187,7 +187,7 @@ def test_tile_vs_numpy_backend(name, domain, tile_by):
     ref = {k: v.copy() for k, v in arrays.items()}
     _stencil(name, "numpy")(**ref, origin=origins, domain=domain)
     st = _stencil(name, "gt:mi355x", tile_by=tile_by)
-    dev = {k: storage.from_array(v, backend="gt:mi355x", aligned_index=origins[k]) for k, v in arrays.items()}
+    dev = {k: storage.from_array(v, v.dtype, backend="gt:mi355x", aligned_index=origins[k]) for k, v in arrays.items()}
     st(**dev, origin=origins, domain=domain)
     got = storage.to_numpy(dev["out"])
     np.testing.assert_array_equal(got, ref["out"])
