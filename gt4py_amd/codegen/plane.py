@@ -584,7 +584,7 @@ class PlaneGen:
                 for a in range(v.depth - 1, 0, -1):
                     for e in range(V):
                         S.append(f"{v.c}_{a}_{e} = {v.c}_{a - 1}_{e};")
-            B.append(f"    {{  // row copy {u}")
+            B.append(f"    {{  // slot copy {u}")
             B.append(f"        const int t = tt + {u};")
             B.append("        if (t >= jce) break;")
             B += ["        " + x for x in S]

@@ -162,7 +162,9 @@ class FrozenStencil:
         src = (
             "def _fast(kwargs):\n"
             + f"    if len(kwargs) != {len(fnames) + len(pnames)}:\n        return False\n"
-            + "".join(f"    {n} = kwargs.get({n!r})\n" for n in fnames + pnames)
+            + "    try:\n"
+            + "".join(f"        {n} = kwargs[{n!r}]\n" for n in fnames + pnames)
+            + "    except KeyError:\n        return False\n"
             + f"    _gt_e = _memo.get({_ids_src(fnames)})\n"
             + f"    return _gt_e is not None and {_fast_check_src(fnames, 1)} and _gt_e[0]({_params_src(pnames)})\n"
         )
@@ -201,6 +203,32 @@ class FrozenStencil:
         if len(self._memo) >= _FAST_MEMO_MAX:
             self._memo.clear()
         self._memo[tuple(id(a) for a in field_args.values())] = (launch, *fields)
+
+
+_UNSET = object()
+
+
+def _frozen_class(fnames, pnames) -> type:
+    """A ``FrozenStencil`` subclass whose ``__call__`` takes the stencil's arguments as named
+    keywords, so a prepared call needs no keyword dict: the fast path of ``FrozenStencil``
+    generated for one argument list (any other call goes to ``FrozenStencil.__call__``)."""
+    names = fnames + pnames
+    params = ", ".join(f"{n}=_UNSET" for n in names)
+    src = (
+        f"def __call__(self, *, {params}{', ' if names else ''}exec_info=None, **_gt_rest):\n"
+        f"    if exec_info is None and not _gt_rest:\n"
+        f"        _gt_e = self._memo.get({_ids_src(fnames)})\n"
+        f"        if _gt_e is not None and {_fast_check_src(fnames, 1)} and _gt_e[0]({_params_src(pnames)}):\n"
+        f"            return\n"
+        f"    _gt_kw = {{k: v for k, v in (" + "".join(f"({n!r}, {n}), " for n in names) + ") if v is not _UNSET}\n"
+        f"    if exec_info is not None:\n"
+        f"        _gt_kw['exec_info'] = exec_info\n"
+        f"    _gt_kw.update(_gt_rest)\n"
+        f"    return _FrozenStencil.__call__(self, **_gt_kw)\n"
+    )
+    ns: Dict[str, Any] = {"_UNSET": _UNSET, "_FrozenStencil": FrozenStencil}
+    exec(compile(src, "<gt4py_amd:FrozenStencil.__call__>", "exec"), ns)  # noqa: S102 - generated code
+    return type("FrozenStencil", (FrozenStencil,), {"__call__": ns["__call__"], "__module__": __name__})
 
 
 class StencilObject(abc.ABC):
@@ -551,7 +579,11 @@ class StencilObject(abc.ABC):
             self.run(_domain_=(ni, rows_b, nk), _origin_=shifted, exec_info=exec_info, **arrays, **parameter_args)
 
     def freeze(self, *, origin: Dict[str, Tuple[int, ...]], domain: Tuple[int, ...]) -> FrozenStencil:
-        return FrozenStencil(self, origin, domain)
+        cls = type(self).__dict__.get("_gt_frozen_cls_")
+        if cls is None:
+            cls = _frozen_class(list(self.field_info), list(self.parameter_info))
+            type.__setattr__(type(self), "_gt_frozen_cls_", cls)
+        return cls(self, origin, domain)
 
     def clean_call_args_cache(self) -> None:
         type(self)._domain_origin_cache.clear()

@@ -114,13 +114,16 @@ def test_halo_library_exports_its_header():
 
 def test_row_unroll_auto_rule():
     """Auto row unroll (plane.py): 4 copies for small register state (lap5), 2 for 4 cells per
-    lane (hdiff f32), none for hdiff f64; the 1-wide fallback variant always stays rolled."""
-    cases = [(sc.lap5, "gpu.unroll_auto_lap5", 4), (sc.hdiff_f32, "gpu.unroll_auto_f32", 2),
-             (sc.hdiff_f64, "gpu.unroll_auto_f64", 0)]
-    for definition, name, u in cases:
+    lane (hdiff f32), none for hdiff f64; the 1-wide fallback variant always stays rolled.
+    The buffer-load strip body (bufld, auto for 4 cells per lane) unrolls by its slot-ring
+    length instead, marked "slot copy"."""
+    cases = [(sc.lap5, "gpu.unroll_auto_lap5", 4, False), (sc.hdiff_f32, "gpu.unroll_auto_f32", 2, True),
+             (sc.hdiff_f64, "gpu.unroll_auto_f64", 0, False)]
+    for definition, name, u, slots in cases:
         st = gtscript.stencil(backend="gt:mi355x", definition=definition, name=name)
         src = open(os.path.join(os.path.dirname(_lib_path(st)), "stencil.hip")).read()
         v1 = src[src.index("k0_plane_v1("):src.index("__global__", src.index("k0_plane_v1("))]
-        assert "// row copy" not in v1
+        assert "// row copy" not in v1 and "// slot copy" not in v1
         copies = set(int(m) for m in re.findall(r"// row copy (\d+)", src))
         assert copies == (set(range(u)) if u else set()), (name, copies)
+        assert ("// slot copy 0" in src) == slots, name
