@@ -54,6 +54,7 @@ CONFIGS = {
     # row 1); algorithmic bytes: `a` read + `out` written
     "staged": ("staged_forward_ij_temp", np.float64, (1024, 1024, 160), 1, 16),
     # shape probes for work-order experiments (scripts/sweep.py; never bench lines)
+    "staged_f32": ("staged_forward_ij_temp", np.float32, (2048, 1024, 160), 1, 8),
     "lap5_k160": ("lap5", np.float64, (1024, 1024, 160), 1, 16),
     "lap5_2k": ("lap5", np.float64, (2048, 2048, 80), 1, 16),
     "copy_k80": ("copy_stencil", np.float64, (1024, 1024, 80), 0, 16),
@@ -174,19 +175,25 @@ def stencil_defs():
                 flx[0, 0, 0] - flx[-1, 0, 0] + fly[0, 0, 0] - fly[0, -1, 0]
             )
 
-    def staged_forward_ij_temp(a: F64, out: F64):
-        # tests/stencil_cases.py staged_forward_ij_temp (golden-pinned)
-        with computation(FORWARD):
-            with interval(0, 1):
-                s = a
-            with interval(1, None):
-                s = s[0, 0, -1] * 0.5 + a
-        with computation(FORWARD), interval(...):
-            t = s * 2.0 + a
-            out = t[1, 0, 0] - t[-1, 0, 0] + t[0, 1, 0] * s
+    def make_staged(dtype):
+        FT = Field[dtype]
+
+        def staged_forward_ij_temp(a: FT, out: FT):
+            # tests/stencil_cases.py staged_forward_ij_temp (golden-pinned)
+            with computation(FORWARD):
+                with interval(0, 1):
+                    s = a
+                with interval(1, None):
+                    s = s[0, 0, -1] * 0.5 + a
+            with computation(FORWARD), interval(...):
+                t = s * 2.0 + a
+                out = t[1, 0, 0] - t[-1, 0, 0] + t[0, 1, 0] * s
+
+        return staged_forward_ij_temp
 
     return {
-        ("staged_forward_ij_temp", np.float64): staged_forward_ij_temp,
+        ("staged_forward_ij_temp", np.float64): make_staged(np.float64),
+        ("staged_forward_ij_temp", np.float32): make_staged(np.float32),
         ("horizontal_diffusion_blocks", np.float64): horizontal_diffusion_blocks,
         ("vertical_advection_dycore", np.float64): vertical_advection_dycore,
         ("horizontal_diffusion", np.float64): make_hdiff(np.float64),

@@ -37,7 +37,7 @@ from gt4py_amd.codegen.common import (  # noqa: F401
 LDS_BYTES = 160 * 1024  # per CU (MI355X_MICROARCH.md); one 256-thread block may take all of it
 DEFAULT_RING = 8
 DEFAULT_KREG = 0  # register band levels (option ``kreg``)
-TILE_BY = 8  # tile mode: J rows of threads per block (64 x 8 = 512 threads, halo included)
+TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
 @dataclasses.dataclass
@@ -90,6 +90,9 @@ class ColumnGen:
             bx, by = self._block()
             if bx - ilo - ihi < 8 or by - jlo - jhi < 1:
                 raise UnsupportedStencil(f"IJ extent {self.ext} too wide for a {bx}x{by} tile")
+            ti = int(opts.get("tile_ti", 0))
+            if ti and not 8 <= ti <= bx - ilo - ihi:
+                raise ValueError(f"tile_ti must be in [8, {bx - ilo - ihi}] for IJ extent {self.ext}, got {ti}")
         self.info = {li: self._analyse_loop(li) for li in kernel.loops}
         self.kreg = 0
         self.tail = None if self.tile else self._plan_tail()
@@ -99,16 +102,47 @@ class ColumnGen:
 
     def _block(self) -> Tuple[int, int]:
         """Threads per block in I and J (option ``col_bx``: I width, 256 threads in total; tile
-        mode: 64 x ``tile_by`` threads, default 8, halo included)."""
+        mode: ``tile_bx`` x ``tile_by`` threads, halo included; defaults 64 x 8 for 8-byte cells,
+        128 x 8 for narrower ones)."""
         if getattr(self.kernel, "tile", False):
             by = int(self.opts.get("tile_by", TILE_BY))
-            if by not in (4, 8, 16):
-                raise ValueError(f"tile_by must be 4, 8 or 16, got {by}")
-            return 64, by
+            # two waves per row for cells of 4 bytes or less (a row of 448 B of outputs, r03l sweep)
+            bx = int(self.opts.get("tile_bx", 0)) or (128 if self._tile_item() <= 4 and by <= 8 else 64)
+            if by not in (4, 8, 16) or bx not in (64, 128) or bx * by > 1024:
+                raise ValueError(f"tile_bx x tile_by must be 64 or 128 x 4, 8 or 16 (at most 1024 threads), got {bx} x {by}")
+            return bx, by
         bx = int(self.opts.get("col_bx", COLUMN_BLOCK[0]))
         if bx not in (64, 128, 256):
             raise ValueError(f"col_bx must be 64, 128 or 256, got {bx}")
         return bx, (COLUMN_BLOCK[0] * COLUMN_BLOCK[1]) // bx
+
+    def _tile_geom(self) -> Tuple[int, int]:
+        """Tile mode: output columns (I) and rows (J) per tile. ``tile_ti`` narrows the I width
+        below the block's 64 lanes minus the halo (lanes past the tile's halo then repeat its
+        last column: same addresses, no extra lines)."""
+        bx, by = self._block()
+        eilo, eihi, ejlo, ejhi = self.ext
+        ti = int(self.opts.get("tile_ti", 0))
+        if not ti:
+            # widest tile whose output rows start on an aligned boundary (128 B for 8-byte cells,
+            # 64 B for narrower ones), so the API stores write whole lines: unaligned 62-wide f64
+            # tiles take 1.2-1.5x the time (profiles/r03/r03l_sweep_tile_geom*.log)
+            ti = bx - eilo - eihi
+            item = self._tile_item()
+            unit = (128 if item >= 8 else 64) // item
+            if ti >= unit:
+                ti -= ti % unit
+        return ti, by - ejlo - ejhi
+
+    def _tile_item(self) -> int:
+        """Largest cell size among the API fields the tile kernel stores (8 if none)."""
+        sizes = set()
+        for li in self.kernel.loops:
+            for sec in self.st.vertical_loops[li].sections:
+                for acc, w in iter_accesses(sec.body):
+                    if w and isinstance(acc, ir.FieldAccess) and acc.name in self.api:
+                        sizes.add(self.st.decl(acc.name).dtype.itemsize)
+        return max(sizes, default=8)
 
     def _guard(self, li, si, ti) -> Optional[str]:
         """Condition restricting top-level statement ti to its own extent (None: whole region)."""
@@ -285,7 +319,9 @@ class ColumnGen:
                         keys.setdefault(acc.name, set()).add(acc.offset[:2])
         self.nt_loads = set()
         self.nt_stores = set()
-        if self.opts.get("nt_load", 1):
+        # tile kernels: the halo lanes load the neighbouring tiles' columns, so every stream is read
+        # by more than one block and stays cacheable (non-temporal: 1.15x the time, r03l sweep)
+        if self.opts.get("nt_load", 0 if self.tile else 1):
             self.nt_loads = {n for n, ks in keys.items() if n not in write_loops and len(ks) == 1 and self._mem(n)}
         if self.opts.get("nt_store", 1):
             self.nt_stores = {
@@ -310,13 +346,16 @@ class ColumnGen:
             # overlapping tiles: block (ti, tj) owns output columns [ti*TI, ti*TI + TI) x
             # [tj*TJ, tj*TJ + TJ) and its threads cover them plus the loop's IJ extent as halo;
             # no thread returns early (every thread reaches every level's barrier)
-            TI, TJ = bx - eilo - eihi, by - ejlo - ejhi
+            TI, TJ = self._tile_geom()
             B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
             B.append("const int b = (int)(blockIdx.y * gridDim.x + blockIdx.x);")
             B.append("const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;")
             B.append("const int w = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;")
             B.append("const int tx = (int)threadIdx.x, ty = (int)threadIdx.y;")
-            B.append(f"const int i = (w % nbx) * {TI} + tx - {eilo};")
+            if TI + eilo + eihi < bx:
+                B.append(f"const int i = (w % nbx) * {TI} + (tx < {TI + eilo + eihi} ? tx : {TI + eilo + eihi - 1}) - {eilo};")
+            else:
+                B.append(f"const int i = (w % nbx) * {TI} + tx - {eilo};")
             B.append(f"const int j = (w / nbx) * {TJ} + ty - {ejlo};")
             B.append(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};")
             B.append(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && ty < {ejlo + TJ} && "
@@ -402,7 +441,7 @@ class ColumnGen:
         else:
             H.append("        p.tail_len = 0;")
         if self.tile:
-            TI, TJ = bx - eilo - eihi, by - ejlo - ejhi
+            TI, TJ = self._tile_geom()
             H.append(
                 f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {TI - 1}) / {TI}), "
                 f"(unsigned)((nj + {TJ - 1}) / {TJ})), dim3({bx}, {by}), {lds}, stream, p);"

@@ -41,16 +41,22 @@ def main():
     origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
     dom = (ni, nj, nk)
 
-    def timeit(fn, n):
+    def timeit(fn, n, burst=64):
+        # bursts short enough that the GPU queue never fills (a full queue makes the host wait on
+        # the device and turns the number into kernel time); the device drains between bursts,
+        # outside the clock; median over bursts
         for _ in range(50):
             fn()
+        per = []
+        for _ in range(max(1, n // burst)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(burst):
+                fn()
+            per.append((time.perf_counter() - t0) / burst * 1e6)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(n):
-            fn()
-        t1 = time.perf_counter()
-        torch.cuda.synchronize()
-        return (t1 - t0) / n * 1e6
+        per.sort()
+        return per[len(per) // 2]
 
     class _Res(dict):
         def __setitem__(self, k, v):
@@ -84,7 +90,7 @@ def main():
             st(fin, out, coeff, origin=origin, domain=dom, validate_args=False)
 
     g = StencilGraph(ten)
-    res["graph_replay_per_call"] = timeit(g.replay, max(1, args.calls // 10)) / 10
+    res["graph_replay_per_call"] = timeit(g.replay, max(1, args.calls // 10), burst=8) / 10
     # GPU time of the tiny kernel itself, for scale
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -93,6 +99,20 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     res["gpu_us_per_launch_backtoback"] = e0.elapsed_time(e1) / 200 * 1e3
+
+    # round trips (call + synchronize each time, the bench's full_call shape): the bare ctypes
+    # launch sets the driver's floor (launch latency + kernel + completion wake-up); the
+    # difference to the validated call is what the Python layers add
+    def rt_ctypes():
+        lib.run(d3, fields, launcher.n_fields, scal, 0, s)
+        torch.cuda.synchronize()
+
+    def rt_call():
+        st(fin, out, coeff, origin=origin, domain=dom, validate_args=True)
+        torch.cuda.synchronize()
+
+    res["roundtrip_ctypes_sync"] = timeit(rt_ctypes, args.calls // 2)
+    res["roundtrip_call_validate_sync"] = timeit(rt_call, args.calls // 2)
 
 
 if __name__ == "__main__":

@@ -88,6 +88,10 @@ def tile_f32(a: F32, out: F32):
         out = t[1, 1, 0] - t[-1, -1, 0]
 
 
+# (tile_by, tile_ti, tile_bx): block rows, tile width in I and block lanes in I (0: defaults,
+# the aligned tile width and 64 or 128 lanes by cell size)
+GEOMS = [(8, 0, 0), (4, 0, 0), (16, 0, 0), (8, 60, 64), (16, 13, 0), (4, 0, 128), (8, 100, 128)]
+
 # name: (definition, {field: (halo_i_lo, halo_i_hi, halo_j_lo, halo_j_hi)}, dtype)
 CASES = {
     "fwd_recurrence_ij_temp": (fwd_recurrence_ij_temp, {"a": (1, 1, 0, 1)}, np.float64),
@@ -175,8 +179,8 @@ def _inputs(name, domain, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(CASES))
 @pytest.mark.parametrize("domain", [(5, 3, 4), (70, 9, 6), (131, 23, 13)])
-@pytest.mark.parametrize("tile_by", [8, 4, 16])
-def test_tile_vs_numpy_backend(name, domain, tile_by):
+@pytest.mark.parametrize("geom", GEOMS)
+def test_tile_vs_numpy_backend(name, domain, geom):
     import torch
 
     if not torch.cuda.is_available():
@@ -186,7 +190,8 @@ def test_tile_vs_numpy_backend(name, domain, tile_by):
     arrays, origins = _inputs(name, domain, seed=sum(domain))
     ref = {k: v.copy() for k, v in arrays.items()}
     _stencil(name, "numpy")(**ref, origin=origins, domain=domain)
-    st = _stencil(name, "gt:mi355x", tile_by=tile_by)
+    tile_by, tile_ti, tile_bx = geom
+    st = _stencil(name, "gt:mi355x", tile_by=tile_by, tile_ti=tile_ti, tile_bx=tile_bx)
     dev = {k: storage.from_array(v, v.dtype, backend="gt:mi355x", aligned_index=origins[k]) for k, v in arrays.items()}
     st(**dev, origin=origins, domain=domain)
     got = storage.to_numpy(dev["out"])
