@@ -90,9 +90,9 @@ class _Compiled:
             rows=rows,
         )
 
-    def bind(self, domain, origin, arrays, param_names):
+    def bind(self, domain, origin, arrays, param_names, tensors):
         """Prepared launch for the StencilObject fast path (``StencilLauncher.bind``)."""
-        return self.launcher.bind(domain, origin, arrays, param_names,
+        return self.launcher.bind(domain, origin, arrays, param_names, tensors,
                                   device_sync=bool(self.options.get("device_sync", True)))
 
 

@@ -59,6 +59,18 @@ def _np_dtype_of(t) -> np.dtype:
     return numpy_dtype_of(t)
 
 
+# dtype name -> scalar kind of the native prepared launch (csrc/gtmi_fastcall.cpp, enum Kind)
+_SCALAR_KIND = {"float64": 0, "float32": 1, "int64": 2, "int32": 3, "int16": 4, "int8": 5, "bool": 6}
+_SCALAR_TYPES = (float, int, bool, np.float64, np.float32, np.int64, np.int32, np.int16, np.int8, np.bool_)
+
+
+def _exact_types(dtype_name: str) -> tuple:
+    """The Python scalar types a validated call accepts for a parameter of this dtype: those whose
+    numpy dtype is the parameter's (the reference's check, stencil_object.py:481-489)."""
+    want = np.dtype(dtype_name)
+    return tuple(t for t in _SCALAR_TYPES if np.dtype(t) == want)
+
+
 class StencilLauncher:
     def __init__(self, lib_path: str, name: str = ""):
         self.lib_path = lib_path
@@ -197,19 +209,23 @@ class StencilLauncher:
             f.dtype = ffi.DTYPE_IDS[np.dtype(dt).name]
         return fields, device, refs, ptrs
 
-    def bind(self, domain, origin, arrays: Dict[str, Any], param_names, *, device_sync=True):
+    def bind(self, domain, origin, arrays: Dict[str, Any], param_names, tensors, *, device_sync=True):
         """A prepared launch for repeated calls with these arrays, origins and domain: the fast
-        path of ``StencilObject.__call__`` / ``FrozenStencil.__call__`` (the caller checks that
-        the arrays are still the same objects with the same data pointers and shapes).
+        path of ``StencilObject.__call__`` / ``FrozenStencil.__call__``.
 
-        Returns ``launch(params) -> bool`` (``params``: the scalar values in ``param_names``
-        order; False when the call must take the ordinary path, e.g. another current device),
-        or None when this call cannot be prepared. Everything a call does not change -- the
-        packed ``gtmi_field`` array, the domain, the scalar slots, the foreign function -- is
-        built here once; a launch sets the scalars, reads torch's current raw stream and makes
-        the one foreign call.
+        ``tensors``: the field arguments in call order (plain torch tensors). Returns
+        ``launch(fields, params) -> bool`` -- ``fields`` the field arguments of a call in the same
+        order, ``params`` its scalar values in ``param_names`` order -- which launches and returns
+        True when every field is still the same tensor (same object, data pointer and sizes) and
+        the current device is the arrays' one, else returns False (take the ordinary path); or
+        None when this call cannot be prepared. Everything a call does not change (the packed
+        ``gtmi_field`` array, the domain, the scalar slots, the foreign function) is built here
+        once. With the native extension (``runtime/fastcall.py``) the whole launch is one C++
+        call; without it, a ctypes closure does the same.
         """
         import torch
+
+        from gt4py_amd.runtime import fastcall
 
         lib = self.lib
         fields, device = self.pack_fields(domain, origin, arrays)
@@ -221,24 +237,46 @@ class StencilLauncher:
         setters = []
         for j, s in enumerate(self.scalars):
             if s["name"] in param_names:
-                attr, conv = ffi.SCALAR_SLOTS[s["dtype"]]
-                setters.append((scalars[j], param_names.index(s["name"]), attr, conv))
+                # a parameter the stencil never reads is not type-checked by validation either
+                setters.append((param_names.index(s["name"]), j, s["dtype"], s.get("used", True)))
             elif s.get("used", True):
                 return None
             else:
                 ffi.set_scalar(scalars[j], s["dtype"], 0)
         ni, nj, nk = (int(d) for d in domain)
+        name = self.name
+        native = fastcall.module()
+        if native is not None:
+            return native.Prepared(
+                ctypes.cast(lib.run, ctypes.c_void_p).value, ctypes.cast(lib.lib.gtmi_last_error, ctypes.c_void_p).value,
+                (ni, nj, nk), ctypes.addressof(fields), self.n_fields, ctypes.addressof(scalars), n_sc,
+                [(pos, j, _SCALAR_KIND[dt], _exact_types(dt) if used else ()) for pos, j, dt, used in setters],
+                len(param_names),
+                list(tensors), idx,
+                bool(device_sync), name)
+        import weakref
+
         dom = (ctypes.c_int64 * 3)(ni, nj, nk)
         run = lib.run
         n_fields = self.n_fields
         raw_stream = torch._C._cuda_getCurrentRawStream
         current_device = torch._C._cuda_getDevice
-        name = self.name
+        slots = [(scalars[j], pos, *ffi.SCALAR_SLOTS[dt], _exact_types(dt) if used else ())
+                 for pos, j, dt, used in setters]
+        checks = [(weakref.ref(t), t.data_ptr(), t.shape) for t in tensors]
+        n_params = len(param_names)
 
-        def launch(params) -> bool:
+        def launch(fields_now, params, strict) -> bool:
+            if len(fields_now) != len(checks) or len(params) != n_params:
+                return False
+            for a, (ref, ptr, shape) in zip(fields_now, checks):
+                if ref() is not a or a.data_ptr() != ptr or a.shape != shape:
+                    return False
             if current_device() != idx:
                 return False
-            for slot, pos, attr, conv in setters:
+            if strict and any(exact and type(params[pos]) not in exact for _, pos, _, _, exact in slots):
+                return False
+            for slot, pos, attr, conv, _ in slots:
                 setattr(slot, attr, conv(params[pos]))
             rc = run(dom, fields, n_fields, scalars, n_sc, raw_stream(idx))
             if rc != 0:

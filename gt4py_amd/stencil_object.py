@@ -106,39 +106,30 @@ def _plain_value(v) -> bool:
     return False
 
 
-def _fast_entry_fields(field_args, arrays):
-    """``(weakref, data_ptr, shape)`` per field argument, or None when a field is not a plain
-    torch tensor passed through unchanged (no gt4py dims/origin metadata, no view made)."""
+def _fast_tensors(field_args, arrays):
+    """The field arguments (call order) when a fast-path entry can be made for them: every one a
+    plain CUDA torch tensor passed through unchanged (no gt4py dims/origin metadata, no view
+    made); else None. The prepared launch re-checks object, data pointer and sizes per call."""
     try:
         import torch
     except ImportError:  # pragma: no cover
         return None
     out = []
-    import weakref
-
     for name, a in field_args.items():
         if type(a) is not torch.Tensor or arrays.get(name) is not a or not a.is_cuda:
             return None
         if getattr(a, "__gt_dims__", None) is not None or getattr(a, "__gt_origin__", None) is not None:
             return None
-        out += [weakref.ref(a), a.data_ptr(), a.shape]
+        out.append(a)
     return out
 
 
-def _fast_check_src(field_names, base: int) -> str:
-    conds = []
-    for i, n in enumerate(field_names):
-        b = base + 3 * i
-        conds += [f"_gt_e[{b}]() is {n}", f"{n}.data_ptr() == _gt_e[{b + 1}]", f"{n}.shape == _gt_e[{b + 2}]"]
-    return " and ".join(conds) or "True"
+def _tuple_src(names) -> str:
+    return "(" + "".join(f"{n}, " for n in names) + ")"
 
 
 def _ids_src(field_names) -> str:
     return "(" + "".join(f"id({n}), " for n in field_names) + ")"
-
-
-def _params_src(param_names) -> str:
-    return "(" + "".join(f"{n}, " for n in param_names) + ")"
 
 
 @dataclass(frozen=True)
@@ -155,7 +146,7 @@ class FrozenStencil:
                 raise ValueError(
                     f"'{name}' origin {self.origin.get(name)} is not a {field_info.ndim}-dimensional integer tuple"
                 )
-        # fast path (see _fast_entry_fields): entry = (launch, weakref, data_ptr, shape, ...)
+        # fast path (see _fast_tensors): entry = prepared launch(fields, params) -> bool
         fnames = list(self.stencil_object.field_info.keys())
         pnames = list(self.stencil_object.parameter_info.keys())
         memo: Dict[tuple, tuple] = {}
@@ -166,7 +157,7 @@ class FrozenStencil:
             + "".join(f"        {n} = kwargs[{n!r}]\n" for n in fnames + pnames)
             + "    except KeyError:\n        return False\n"
             + f"    _gt_e = _memo.get({_ids_src(fnames)})\n"
-            + f"    return _gt_e is not None and {_fast_check_src(fnames, 1)} and _gt_e[0]({_params_src(pnames)})\n"
+            + f"    return _gt_e is not None and _gt_e({_tuple_src(fnames)}, {_tuple_src(pnames)}, False)\n"
         )
         ns: Dict[str, Any] = {"_memo": memo}
         exec(compile(src, "<gt4py_amd:FrozenStencil._fast>", "exec"), ns)  # noqa: S102 - generated code
@@ -194,15 +185,15 @@ class FrozenStencil:
         bind = getattr(type(self.stencil_object)._gt_run_impl_, "bind", None)
         if bind is None or any(a is None for a in field_args.values()):
             return
-        fields = _fast_entry_fields(field_args, field_args)
-        if fields is None:
+        tensors = _fast_tensors(field_args, field_args)
+        if tensors is None:
             return
-        launch = bind(self.domain, self.origin, field_args, tuple(parameter_args))
+        launch = bind(self.domain, self.origin, field_args, tuple(parameter_args), tensors)
         if launch is None:
             return
         if len(self._memo) >= _FAST_MEMO_MAX:
             self._memo.clear()
-        self._memo[tuple(id(a) for a in field_args.values())] = (launch, *fields)
+        self._memo[tuple(id(a) for a in tensors)] = launch
 
 
 _UNSET = object()
@@ -218,7 +209,7 @@ def _frozen_class(fnames, pnames) -> type:
         f"def __call__(self, *, {params}{', ' if names else ''}exec_info=None, **_gt_rest):\n"
         f"    if exec_info is None and not _gt_rest:\n"
         f"        _gt_e = self._memo.get({_ids_src(fnames)})\n"
-        f"        if _gt_e is not None and {_fast_check_src(fnames, 1)} and _gt_e[0]({_params_src(pnames)}):\n"
+        f"        if _gt_e is not None and _gt_e({_tuple_src(fnames)}, {_tuple_src(pnames)}, False):\n"
         f"            return\n"
         f"    _gt_kw = {{k: v for k, v in (" + "".join(f"({n!r}, {n}), " for n in names) + ") if v is not _UNSET}\n"
         f"    if exec_info is not None:\n"
@@ -531,7 +522,7 @@ class StencilObject(abc.ABC):
             exec_info["call_run_end_time"] = time.perf_counter()
 
     def _remember_call(self, field_args, parameter_args, user_domain, user_origin, domain, origin, arrays) -> None:
-        """Make the fast-path entry of this call signature (see ``_fast_entry_fields``)."""
+        """Make the fast-path entry of this call signature (see ``_fast_tensors``)."""
         cls = type(self)
         memo = cls.__dict__.get("_gt_fast_memo_")
         bind = getattr(cls._gt_run_impl_, "bind", None)
@@ -539,18 +530,17 @@ class StencilObject(abc.ABC):
             return
         if not (_plain_value(user_domain) and _plain_value(user_origin)):
             return
-        fields = _fast_entry_fields(field_args, arrays)
-        if fields is None:
+        tensors = _fast_tensors(field_args, arrays)
+        if tensors is None:
             return
-        launch = bind(domain, origin, arrays, tuple(parameter_args))
+        launch = bind(domain, origin, arrays, tuple(parameter_args), tensors)
         if launch is None:
             return
         import copy
 
         if len(memo) >= _FAST_MEMO_MAX:
             memo.clear()
-        memo[tuple(id(a) for a in field_args.values())] = (
-            copy.deepcopy(user_domain), copy.deepcopy(user_origin), launch, *fields)
+        memo[tuple(id(a) for a in tensors)] = (copy.deepcopy(user_domain), copy.deepcopy(user_origin), launch)
 
     def _run_rows(self, domain, origin, exec_info, arrays, parameter_args, j_split, j_skip):
         ni, nj, nk = domain
@@ -652,7 +642,7 @@ def make_stencil_class(
     parts += ["domain=None", "origin=None", "validate_args=True", "exec_info=None"]
     fdict = ", ".join(f"{n}={n}" for n in field_names)
     pdict = ", ".join(f"{n}={n}" for n in param_names)
-    # fast path (see _fast_entry_fields): entry = (domain, origin, launch, weakref, data_ptr, shape, ...)
+    # fast path (see _fast_tensors): entry = (domain, origin, prepared launch(fields, params) -> bool)
     memo: Dict[tuple, tuple] = {}
     ns["_memo"] = memo
     src = (
@@ -660,7 +650,7 @@ def make_stencil_class(
         f"    if exec_info is None:\n"
         f"        _gt_e = _memo.get({_ids_src(field_names)})\n"
         f"        if _gt_e is not None and _gt_e[0] == domain and _gt_e[1] == origin and "
-        f"{_fast_check_src(field_names, 3)} and _gt_e[2]({_params_src(param_names)}):\n"
+        f"_gt_e[2]({_tuple_src(field_names)}, {_tuple_src(param_names)}, validate_args):\n"
         f"            return\n"
         f"    self._call_impl(dict({fdict}), dict({pdict}), domain, origin, validate_args, exec_info)\n"
     )

@@ -4,6 +4,7 @@
     python scripts/call_overhead.py [--calls 3000]
 
 Prints one JSON line per layer: StencilObject.__call__ with validation, without, FrozenStencil,
+the prepared launch they end in (native, and the same calls with the ctypes closure instead),
 the launcher alone, and the bare ``gtmi_stencil_run`` ctypes call on pre-packed arguments.
 ``device_sync=False`` everywhere: the number is host time per enqueued call.
 """
@@ -69,6 +70,22 @@ def main():
         lambda: st(fin, out, coeff, origin=origin, domain=dom, validate_args=False), args.calls)
     frozen = st.freeze(origin=origin, domain=dom)
     res["frozen"] = timeit(lambda: frozen(in_field=fin, out_field=out, coeff=coeff), args.calls)
+    (entry,) = type(st)._gt_fast_memo_.values()
+    prepared = entry[2]  # what the cached __call__ ends in (native Prepared, or the ctypes closure)
+    print(json.dumps({"prepared_kind": type(prepared).__name__}), flush=True)
+    res["prepared_only"] = timeit(lambda: prepared((fin, out, coeff), (), False), args.calls)
+    from gt4py_amd.runtime import fastcall
+
+    native = fastcall.module()
+    if native is not None:  # the same layers with the launcher's ctypes closure instead
+        fastcall._module = None
+        st.clean_call_args_cache()
+        res["call_validate_ctypes_closure"] = timeit(lambda: st(fin, out, coeff, origin=origin, domain=dom),
+                                                     args.calls)
+        frozen_c = st.freeze(origin=origin, domain=dom)
+        res["frozen_ctypes_closure"] = timeit(lambda: frozen_c(in_field=fin, out_field=out, coeff=coeff), args.calls)
+        fastcall._module = native
+        st.clean_call_args_cache()
     comp = [c.cell_contents for c in type(st).run.__closure__][0].compiled
     launcher = comp.launcher
     arrays = {"in_field": fin, "out_field": out, "coeff": coeff}

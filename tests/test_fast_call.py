@@ -3,7 +3,8 @@
 domain and origin skips argument extraction and packing. These tests pin that it never changes
 results: scalar parameters are re-read on every call, swapped / re-allocated / re-pointed
 (``set_``) / re-shaped arrays and changed domains or origins take the ordinary path, and
-``exec_info`` calls keep their timestamps. Every case is checked against numpy.
+``exec_info`` calls keep their timestamps. Every case is checked against numpy, once with the
+native prepared launch (``csrc/gtmi_fastcall.cpp``) and once with the launcher's ctypes closure.
 """
 
 import numpy as np
@@ -13,9 +14,21 @@ from gt4py_amd import gtscript
 from gt4py_amd import storage as gt_storage
 from gt4py_amd.gtscript import PARALLEL, Field, computation, interval
 
-pytestmark = pytest.mark.gpu
-
 BK = "gt:mi355x"
+
+
+@pytest.fixture(params=["native", "ctypes"])
+def mode(request, monkeypatch):
+    from gt4py_amd.runtime import fastcall
+
+    if request.param == "ctypes":
+        monkeypatch.setattr(fastcall, "_module", None)
+        monkeypatch.setattr(fastcall, "_tried", True)
+    elif fastcall.module() is None:
+        pytest.skip("gt4py_amd._gtmi_fastcall not built")
+    return request.param
+
+
 
 
 def _need_gpu():
@@ -52,6 +65,8 @@ def _memo(st):
     return type(st)._gt_fast_memo_
 
 
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
 def test_repeated_calls_hit_and_reread_scalars():
     _need_gpu()
     st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
@@ -64,6 +79,8 @@ def test_repeated_calls_hit_and_reread_scalars():
     assert len(_memo(st)) == 1
 
 
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
 def test_swapped_and_new_arrays():
     _need_gpu()
     st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
@@ -85,6 +102,8 @@ def test_swapped_and_new_arrays():
         del a, b
 
 
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
 def test_set_and_resize_take_the_ordinary_path():
     _need_gpu()
     import torch
@@ -105,6 +124,8 @@ def test_set_and_resize_take_the_ordinary_path():
     torch.cuda.synchronize()
 
 
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
 def test_domain_and_origin_changes():
     _need_gpu()
     st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
@@ -126,9 +147,12 @@ def test_domain_and_origin_changes():
                                   _expect(a, 2.0, (5, 4, 3), (1, 2, 1), (0, 0, 0), b_init=np.zeros(full)))
 
 
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
 def test_exec_info_after_fast_calls():
     _need_gpu()
     st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
     a, b = _fields(6)
     for _ in range(3):
         st(a, b, w=1.0, domain=(17, 9, 5), origin=(0, 0, 0))
@@ -138,6 +162,8 @@ def test_exec_info_after_fast_calls():
         assert k in info
 
 
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
 def test_frozen_fast_path():
     _need_gpu()
     st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
@@ -154,3 +180,72 @@ def test_frozen_fast_path():
     info = {}
     fz(a=a2, b=b2, w=3.0, exec_info=info)
     assert "call_run_start_time" in info and "run_cpp_start_time" in info
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
+def test_parameter_types_and_entry_kind(mode):
+    """Validated calls keep the reference's parameter type check on the fast path (a float32
+    value for a float64 parameter raises TypeError even with an entry made); unvalidated calls
+    convert numpy scalars, ints and bools as the ordinary path does. The memo entry is the
+    native Prepared object when the extension is built."""
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    a, b = _fields(10)
+    dom = (17, 9, 5)
+    st(a, b, w=0.5, domain=dom, origin=(0, 0, 0))
+    (entry,) = _memo(st).values()
+    assert (type(entry[2]).__name__ == "Prepared") == (mode == "native")
+    for bad in (np.float32(1.5), 2, True):
+        with pytest.raises(TypeError):
+            st(a, b, w=bad, domain=dom, origin=(0, 0, 0))
+    for w in (np.float32(1.5), 2, np.float64(-0.25), np.int64(3), True, 0.125):
+        st(a, b, w=w, domain=dom, origin=(0, 0, 0), validate_args=False)
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a, float(w), dom, b_init=np.zeros(dom)))
+    fz = st.freeze(origin={"a": (0, 0, 0), "b": (0, 0, 0)}, domain=dom)
+    for w in (0.5, np.float32(2.5), 4):  # FrozenStencil never validates (reference :94-128)
+        fz(a=a, b=b, w=w)
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a, float(w), dom, b_init=np.zeros(dom)))
+
+
+def test_native_prepared_rejects_other_arguments():
+    """CPU: a Prepared launch returns False (no launch) for other tensors, a re-pointed tensor,
+    another argument count or a wrong container -- every path that never reaches the library."""
+    import ctypes
+
+    import torch
+
+    from gt4py_amd.runtime import fastcall, ffi
+
+    m = fastcall.module()
+    if m is None:
+        pytest.skip("gt4py_amd._gtmi_fastcall not built")
+    x, y = torch.zeros(4, 3, 2), torch.zeros(4, 3, 2)
+    fields = (ffi.GtmiField * 2)()
+    scal = (ffi.GtmiScalar * 1)()
+    p = m.Prepared(0, 0, (4, 3, 2), ctypes.addressof(fields), 2, ctypes.addressof(scal), 1,
+                   [(0, 0, 0, (float, np.float64))], 1, [x, y], 0, False, "t")
+    assert p((y, x), (1.0,), True) is False  # swapped
+    assert p((x,), (1.0,), True) is False  # too few fields
+    assert p((x, y), (), True) is False  # too few params
+    assert p([x, y], (1.0,), True) is False  # not a tuple
+    y.set_(torch.zeros(4, 3, 2).untyped_storage())
+    assert p((x, y), (1.0,), True) is False  # same object, new data
+    with pytest.raises(TypeError):
+        p((x, y), (1.0,))  # strict flag missing
+    with pytest.raises(ValueError):
+        m.Prepared(0, 0, (4, 3, 2), ctypes.addressof(fields), 2, ctypes.addressof(scal), 1, [(5, 0, 0, ())], 1,
+                   [x, y], 0, False, "t")
+    with pytest.raises(TypeError):
+        m.Prepared(0, 0, (4, 3, 2), ctypes.addressof(fields), 2, ctypes.addressof(scal), 1, [(0, 0, 0, (1,))], 1,
+                   [x, y], 0, False, "t")
+
+
+def test_exact_parameter_types():
+    from gt4py_amd.runtime.launcher import _exact_types
+
+    assert set(_exact_types("float64")) == {float, np.float64}
+    assert set(_exact_types("float32")) == {np.float32}
+    assert set(_exact_types("int64")) == {int, np.int64}
+    assert set(_exact_types("bool")) == {bool, np.bool_}
