@@ -7,17 +7,17 @@
 // signature needs -- the packed gtmi_field array, the domain, the scalar slots and the
 // library's gtmi_stencil_run -- and a call
 //
-//     prepared(fields: tuple, params: tuple, strict: bool) -> bool
+//     prepared(fields: tuple, params: tuple) -> bool
 //
 // checks that every field argument is still the tensor the entry was made for (same object via
-// its weak reference, same data pointer, same sizes), stores the scalar parameters, reads the
-// caller's current HIP stream from c10 and launches. With `strict` (a validated call) every
-// parameter's type must be one whose numpy dtype is the declared one, as the reference's
-// _validate_args demands (stencil_object.py:481-489); otherwise the ordinary path's conversions
-// apply. False means "take the ordinary path" (another tensor, another current device, a
-// parameter that validation or conversion would treat differently); a failing launch raises
-// RuntimeError with gtmi_last_error(). The GIL is held during the (non-blocking) launch, as the
-// reference's binding does.
+// its weak reference, same data pointer, same sizes), stores the scalar parameters with the
+// ordinary path's conversions, reads the caller's current HIP stream from c10 and launches.
+// Parameter values are not re-validated, as in the reference, whose _validate_args runs only
+// when the (shapes, origins, parameter names, domain) cache misses (stencil_object.py:578-591).
+// False means "take the ordinary path" (another tensor, another current device, a parameter the
+// conversions would treat differently); a failing launch raises RuntimeError with
+// gtmi_last_error(). The GIL is held during the (non-blocking) launch, as the reference's
+// binding does.
 #include <Python.h>
 
 #include <c10/hip/HIPFunctions.h>
@@ -42,7 +42,6 @@ struct Setter {
     int pos;   // index in the params tuple
     int slot;  // gtmi_scalar slot
     int kind;
-    std::vector<PyObject*> exact;  // types whose numpy dtype is the parameter's (owned; empty: any)
 };
 
 struct Check {
@@ -103,14 +102,12 @@ bool set_scalar(gtmi_scalar& s, int kind, PyObject* v) {
 PyObject* prepared_call(PyObject* self_, PyObject* args, PyObject* kwargs) {
     Prepared* self = (Prepared*)self_;
     PyObject *fields, *params;
-    if (kwargs || PyTuple_GET_SIZE(args) != 3) {
-        PyErr_SetString(PyExc_TypeError, "prepared launch takes (fields, params, strict)");
+    if (kwargs || PyTuple_GET_SIZE(args) != 2) {
+        PyErr_SetString(PyExc_TypeError, "prepared launch takes (fields, params)");
         return nullptr;
     }
     fields = PyTuple_GET_ITEM(args, 0);
     params = PyTuple_GET_ITEM(args, 1);
-    const int strict = PyObject_IsTrue(PyTuple_GET_ITEM(args, 2));
-    if (strict < 0) return nullptr;
     if (!PyTuple_Check(fields) || !PyTuple_Check(params)) Py_RETURN_FALSE;
     const std::vector<Check>& checks = *self->checks;
     if ((size_t)PyTuple_GET_SIZE(fields) != checks.size() || PyTuple_GET_SIZE(params) != self->n_params)
@@ -127,15 +124,8 @@ PyObject* prepared_call(PyObject* self_, PyObject* args, PyObject* kwargs) {
     }
     if ((int)c10::hip::current_device() != self->device) Py_RETURN_FALSE;
     gtmi_scalar* sc = self->scalars->data();
-    for (const Setter& s : *self->setters) {
-        PyObject* v = PyTuple_GET_ITEM(params, s.pos);
-        if (strict && !s.exact.empty()) {
-            bool ok = false;
-            for (PyObject* t : s.exact) ok = ok || (PyObject*)Py_TYPE(v) == t;
-            if (!ok) Py_RETURN_FALSE;
-        }
-        if (!set_scalar(sc[s.slot], s.kind, v)) Py_RETURN_FALSE;
-    }
+    for (const Setter& s : *self->setters)
+        if (!set_scalar(sc[s.slot], s.kind, PyTuple_GET_ITEM(params, s.pos))) Py_RETURN_FALSE;
     hipStream_t stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)self->device).stream();
     int rc = self->run(self->dom, self->fields->data(), (int32_t)self->fields->size(), sc, self->n_scalars,
                        (void*)stream);
@@ -160,9 +150,6 @@ void prepared_dealloc(PyObject* self_) {
     Prepared* self = (Prepared*)self_;
     if (self->checks)
         for (Check& c : *self->checks) Py_XDECREF(c.wr);
-    if (self->setters)
-        for (Setter& st : *self->setters)
-            for (PyObject* t : st.exact) Py_DECREF(t);
     delete self->fields;
     delete self->scalars;
     delete self->setters;
@@ -172,8 +159,7 @@ void prepared_dealloc(PyObject* self_) {
 }
 
 // Prepared(run_addr, err_addr, domain(3), fields_addr, n_fields, scalars_addr (max(1, n) slots), n_scalars,
-//          setters: [(param_pos, slot, kind, (exact types...))], n_params, tensors: [tensor], device,
-//          sync, name)
+//          setters: [(param_pos, slot, kind)], n_params, tensors: [tensor], device, sync, name)
 // The field and scalar arrays are copied: the ctypes objects they come from need not outlive it.
 PyObject* prepared_new(PyTypeObject* type, PyObject* args, PyObject* kwargs) {
     unsigned long long run_addr, err_addr, fields_addr, scal_addr;
@@ -208,23 +194,12 @@ PyObject* prepared_new(PyTypeObject* type, PyObject* args, PyObject* kwargs) {
     self->name = name;
     for (Py_ssize_t i = 0; i < PyList_GET_SIZE(setters); ++i) {
         Setter s;
-        PyObject* exact;
-        if (!PyArg_ParseTuple(PyList_GET_ITEM(setters, i), "iiiO!", &s.pos, &s.slot, &s.kind, &PyTuple_Type, &exact))
-            goto fail;
+        if (!PyArg_ParseTuple(PyList_GET_ITEM(setters, i), "iii", &s.pos, &s.slot, &s.kind)) goto fail;
         if (s.pos < 0 || s.pos >= n_params || s.slot < 0 || s.slot >= n_sc || s.kind < K_F64 || s.kind > K_BOOL) {
             PyErr_SetString(PyExc_ValueError, "bad scalar setter");
             goto fail;
         }
-        for (Py_ssize_t q = 0; q < PyTuple_GET_SIZE(exact); ++q) {
-            PyObject* t = PyTuple_GET_ITEM(exact, q);
-            if (!PyType_Check(t)) {
-                PyErr_SetString(PyExc_TypeError, "exact parameter types must be types");
-                goto fail;
-            }
-            Py_INCREF(t);
-            s.exact.push_back(t);
-        }
-        self->setters->push_back(std::move(s));
+        self->setters->push_back(s);
     }
     for (Py_ssize_t i = 0; i < PyList_GET_SIZE(tensors); ++i) {
         PyObject* t = PyList_GET_ITEM(tensors, i);
@@ -260,7 +235,7 @@ PyMODINIT_FUNC PyInit__gtmi_fastcall(void) {
     PreparedType.tp_new = prepared_new;
     PreparedType.tp_dealloc = prepared_dealloc;
     PreparedType.tp_call = prepared_call;
-    PreparedType.tp_doc = "Prepared(...)(fields, params, strict) -> bool: a launch prepared for one call signature";
+    PreparedType.tp_doc = "Prepared(...)(fields, params) -> bool: a launch prepared for one call signature";
     if (PyType_Ready(&PreparedType) < 0) return nullptr;
     PyObject* m = PyModule_Create(&module_def);
     if (!m) return nullptr;
@@ -270,6 +245,6 @@ PyMODINIT_FUNC PyInit__gtmi_fastcall(void) {
         Py_DECREF(m);
         return nullptr;
     }
-    PyModule_AddIntConstant(m, "ABI", 2);
+    PyModule_AddIntConstant(m, "ABI", 1);
     return m;
 }

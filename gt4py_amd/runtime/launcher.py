@@ -61,14 +61,6 @@ def _np_dtype_of(t) -> np.dtype:
 
 # dtype name -> scalar kind of the native prepared launch (csrc/gtmi_fastcall.cpp, enum Kind)
 _SCALAR_KIND = {"float64": 0, "float32": 1, "int64": 2, "int32": 3, "int16": 4, "int8": 5, "bool": 6}
-_SCALAR_TYPES = (float, int, bool, np.float64, np.float32, np.int64, np.int32, np.int16, np.int8, np.bool_)
-
-
-def _exact_types(dtype_name: str) -> tuple:
-    """The Python scalar types a validated call accepts for a parameter of this dtype: those whose
-    numpy dtype is the parameter's (the reference's check, stencil_object.py:481-489)."""
-    want = np.dtype(dtype_name)
-    return tuple(t for t in _SCALAR_TYPES if np.dtype(t) == want)
 
 
 class StencilLauncher:
@@ -237,8 +229,7 @@ class StencilLauncher:
         setters = []
         for j, s in enumerate(self.scalars):
             if s["name"] in param_names:
-                # a parameter the stencil never reads is not type-checked by validation either
-                setters.append((param_names.index(s["name"]), j, s["dtype"], s.get("used", True)))
+                setters.append((param_names.index(s["name"]), j, s["dtype"]))
             elif s.get("used", True):
                 return None
             else:
@@ -250,8 +241,7 @@ class StencilLauncher:
             return native.Prepared(
                 ctypes.cast(lib.run, ctypes.c_void_p).value, ctypes.cast(lib.lib.gtmi_last_error, ctypes.c_void_p).value,
                 (ni, nj, nk), ctypes.addressof(fields), self.n_fields, ctypes.addressof(scalars), n_sc,
-                [(pos, j, _SCALAR_KIND[dt], _exact_types(dt) if used else ()) for pos, j, dt, used in setters],
-                len(param_names),
+                [(pos, j, _SCALAR_KIND[dt]) for pos, j, dt in setters], len(param_names),
                 list(tensors), idx,
                 bool(device_sync), name)
         import weakref
@@ -261,12 +251,11 @@ class StencilLauncher:
         n_fields = self.n_fields
         raw_stream = torch._C._cuda_getCurrentRawStream
         current_device = torch._C._cuda_getDevice
-        slots = [(scalars[j], pos, *ffi.SCALAR_SLOTS[dt], _exact_types(dt) if used else ())
-                 for pos, j, dt, used in setters]
+        slots = [(scalars[j], pos, *ffi.SCALAR_SLOTS[dt]) for pos, j, dt in setters]
         checks = [(weakref.ref(t), t.data_ptr(), t.shape) for t in tensors]
         n_params = len(param_names)
 
-        def launch(fields_now, params, strict) -> bool:
+        def launch(fields_now, params) -> bool:
             if len(fields_now) != len(checks) or len(params) != n_params:
                 return False
             for a, (ref, ptr, shape) in zip(fields_now, checks):
@@ -274,9 +263,7 @@ class StencilLauncher:
                     return False
             if current_device() != idx:
                 return False
-            if strict and any(exact and type(params[pos]) not in exact for _, pos, _, _, exact in slots):
-                return False
-            for slot, pos, attr, conv, _ in slots:
+            for slot, pos, attr, conv in slots:
                 setattr(slot, attr, conv(params[pos]))
             rc = run(dom, fields, n_fields, scalars, n_sc, raw_stream(idx))
             if rc != 0:

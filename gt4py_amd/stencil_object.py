@@ -157,7 +157,7 @@ class FrozenStencil:
             + "".join(f"        {n} = kwargs[{n!r}]\n" for n in fnames + pnames)
             + "    except KeyError:\n        return False\n"
             + f"    _gt_e = _memo.get({_ids_src(fnames)})\n"
-            + f"    return _gt_e is not None and _gt_e({_tuple_src(fnames)}, {_tuple_src(pnames)}, False)\n"
+            + f"    return _gt_e is not None and _gt_e({_tuple_src(fnames)}, {_tuple_src(pnames)})\n"
         )
         ns: Dict[str, Any] = {"_memo": memo}
         exec(compile(src, "<gt4py_amd:FrozenStencil._fast>", "exec"), ns)  # noqa: S102 - generated code
@@ -209,7 +209,7 @@ def _frozen_class(fnames, pnames) -> type:
         f"def __call__(self, *, {params}{', ' if names else ''}exec_info=None, **_gt_rest):\n"
         f"    if exec_info is None and not _gt_rest:\n"
         f"        _gt_e = self._memo.get({_ids_src(fnames)})\n"
-        f"        if _gt_e is not None and _gt_e({_tuple_src(fnames)}, {_tuple_src(pnames)}, False):\n"
+        f"        if _gt_e is not None and _gt_e({_tuple_src(fnames)}, {_tuple_src(pnames)}):\n"
         f"            return\n"
         f"    _gt_kw = {{k: v for k, v in (" + "".join(f"({n!r}, {n}), " for n in names) + ") if v is not _UNSET}\n"
         f"    if exec_info is not None:\n"
@@ -650,7 +650,7 @@ def make_stencil_class(
         f"    if exec_info is None:\n"
         f"        _gt_e = _memo.get({_ids_src(field_names)})\n"
         f"        if _gt_e is not None and _gt_e[0] == domain and _gt_e[1] == origin and "
-        f"_gt_e[2]({_tuple_src(field_names)}, {_tuple_src(param_names)}, validate_args):\n"
+        f"_gt_e[2]({_tuple_src(field_names)}, {_tuple_src(param_names)}):\n"
         f"            return\n"
         f"    self._call_impl(dict({fdict}), dict({pdict}), domain, origin, validate_args, exec_info)\n"
     )

@@ -73,7 +73,7 @@ def main():
     (entry,) = type(st)._gt_fast_memo_.values()
     prepared = entry[2]  # what the cached __call__ ends in (native Prepared, or the ctypes closure)
     print(json.dumps({"prepared_kind": type(prepared).__name__}), flush=True)
-    res["prepared_only"] = timeit(lambda: prepared((fin, out, coeff), (), False), args.calls)
+    res["prepared_only"] = timeit(lambda: prepared((fin, out, coeff), ()), args.calls)
     from gt4py_amd.runtime import fastcall
 
     native = fastcall.module()
