@@ -687,7 +687,7 @@ def main():
                     help="N=1: after the timed K steps, run the step for about this many seconds more and report "
                          "the steady-state ms/step as `sustained` (0 = off)")
     ap.add_argument("--jchunk", type=int, default=None)
-    ap.add_argument("--placement-candidates", type=int, default=3,
+    ap.add_argument("--placement-candidates", type=int, default=5,
                     help="before timing, place the fields the stencil writes in the fastest of this many other "
                          "buffer sets besides the first allocation (gt4py_amd.storage.placement; 0 = off, the "
                          "first allocation is timed)")

@@ -55,3 +55,23 @@ def test_bench_world_size_mismatch_is_an_error():
     res = _run(["--dry-run", "--gpus", "2"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert res.returncode == 2
     assert "WORLD_SIZE" in res.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpu_line_with_placement_tuning():
+    """The real N=1 line on the GPU (small config): one JSON line, roofline within [0, 1], and the
+    written field placed by measurement with every buffer set's time recorded (set 0 = the first
+    allocation, the untuned time)."""
+    res = _run(["--config", "lap5", "--steps", "5", "--warmup", "2", "--no-extra", "--no-cpu-baseline",
+                "--sustain", "0", "--placement-candidates", "2"], timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, res.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 1 and rec["dtype"] == "f64" and rec["unit"] == "Mcells/s"
+    assert 0.0 < rec["roofline"]["frac"] <= 1.0
+    p = rec["placement"]
+    assert p["written"] == ["out_field"] and len(p["candidates_ms"]) == 3
+    assert p["tuned_ms"] == min(p["candidates_ms"]) == p["candidates_ms"][p["chosen"]]
+    assert p["untuned_ms"] == p["candidates_ms"][0]
+    assert rec["full_call"]["overhead_vs"] == "kernel_ms"
