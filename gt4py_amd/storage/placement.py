@@ -16,7 +16,8 @@ the same layout (same strides, same address residue modulo 2 MiB, so alignment a
 stagger of :mod:`gt4py_amd.storage` are preserved), times the call on each set (HIP events,
 median of ``reps`` launches on torch's current stream) and returns the arrays with the written
 fields in the fastest set, holding the contents they had before (restored from a copy: the
-timing launches write them). The report lists every set's time; the unchosen buffers are freed.
+timing launches write them; the caller's original arrays are restored too, also when a call
+raises). The report lists every set's time; the unchosen buffers are freed.
 
 The reference has no counterpart: its storages are plain CuPy/NumPy allocations
 (``/root/reference/src/gt4py/storage/cartesian/interface.py:143-327``); this tool only returns
@@ -104,7 +105,7 @@ def tune_written_fields(
         a.update(sub)
         return lambda: stencil(**a, **params, origin=origin, domain=domain, validate_args=False)
 
-    if not names or candidates <= 0:
+    if not names:  # nothing written: nothing to place (and the call changes no field)
         report["candidates_ms"] = [_time_call(call_with({}), reps)]
         report["untuned_ms"] = report["tuned_ms"] = report["candidates_ms"][0]
         return dict(arrays), report
@@ -113,7 +114,7 @@ def tune_written_fields(
     free, _ = torch.cuda.mem_get_info(arrays[names[0]].device)
     # the backup copy plus the candidate sets must fit in a fraction of what is free
     fit = int(free * memory_fraction // max(per_set, 1)) - 1
-    n_sets = max(0, min(candidates, fit))
+    n_sets = max(0, min(int(candidates), fit))
     report["sets_tried"] = n_sets + 1
     backup = {n: arrays[n].clone() for n in names}
     sets: List[Dict[str, Any]] = [{n: arrays[n] for n in names}]
@@ -122,7 +123,11 @@ def tune_written_fields(
     for s in sets[1:]:
         for n in names:
             s[n].copy_(backup[n])
-    times = [_time_call(call_with(s), reps) for s in sets]
+    try:
+        times = [_time_call(call_with(s), reps) for s in sets]
+    finally:
+        for n in names:  # the caller's own arrays keep their contents whatever happens
+            arrays[n].copy_(backup[n])
     best = min(range(len(times)), key=times.__getitem__)
     chosen = sets[best]
     for n in names:

@@ -79,8 +79,9 @@ def run_case_on_gpu(case, opts=None, tune=0):
         arrays = {k: v for k, v in dev.items() if k in stencil.field_info and v is not None}
         tuned, rep = tune_written_fields(stencil, arrays, params=case.params, candidates=tune, reps=2, **kw)
         assert rep["written"] and len(rep["candidates_ms"]) == tune + 1, rep
-        for k, v in before.items():  # the tuner keeps every field's contents
+        for k, v in before.items():  # the tuner keeps every field's contents, and the caller's arrays'
             gu.assert_match(storage.to_numpy(tuned.get(k, dev[k])), v, name=f"{case.name}:{k} kept")
+            gu.assert_match(storage.to_numpy(dev[k]), v, name=f"{case.name}:{k} original restored")
         dev.update(tuned)
     stencil(**dev, **case.params, **kw)
     return {k: (None if v is None else storage.to_numpy(v)) for k, v in dev.items()}
