@@ -83,13 +83,31 @@ def tune_written_fields(
     shares memory with another argument (re-homing it would break the aliasing) and ``TypeError``
     for non-device arrays; fewer sets are tried when free device memory is short.
     """
+    return tune_fields(stencil, arrays, written_fields(stencil), origin=origin, domain=domain, params=params,
+                       candidates=candidates, reps=reps, memory_fraction=memory_fraction)
+
+
+def tune_fields(
+    stencil,
+    arrays: Dict[str, Any],
+    names: List[str],
+    *,
+    origin=None,
+    domain=None,
+    params: Optional[Dict[str, Any]] = None,
+    candidates: int = 3,
+    reps: int = 10,
+    memory_fraction: float = 0.8,
+) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+    """:func:`tune_written_fields` for an explicit list of field ``names`` (read-only fields may be
+    among them: they are copied into each candidate set the same way)."""
     import torch
 
     params = dict(params or {})
-    names = written_fields(stencil)
+    names = list(names)
     missing = [n for n in names if n not in arrays]
     if missing:
-        raise ValueError(f"tune_written_fields: written field(s) {missing} not among the arrays")
+        raise ValueError(f"tune_written_fields: field(s) {missing} not among the arrays")
     for n in names:
         t = arrays[n]
         if not (isinstance(t, torch.Tensor) and t.is_cuda):
