@@ -284,6 +284,8 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
     else:
         return {}
 
+    spent = [0.0]
+
     def median_s(f):
         for _ in range(warm):
             f()
@@ -292,9 +294,11 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
             t0 = time.perf_counter()
             f()
             ts.append(time.perf_counter() - t0)
+        spent[0] += sum(ts)
         return float(np.median(ts))
 
     med = median_s(fn)
+    timed_s = spent[0]
     cells = ni * nj * nk
     affinity = int(os.environ.get("GTMI_PARENT_AFFINITY", "0")) or None
     rec = {
@@ -305,6 +309,7 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
         "os_cpu_count": os.cpu_count(),
         "kind": "port",
         "ms_per_call": round(med * 1e3, 3),
+        "timed_s": round(timed_s, 2),
         "cpu_model": _cpu_model(),
         "sample": (f"cpu_ifirst-equivalent (own C++/OpenMP restatement, oracle/cpu_stencils.c) on the full "
                    f"{ni}x{nj}x{nk} {np.dtype(dtype).name} domain ({inputs}); median of {reps} calls after {warm} "
@@ -318,7 +323,7 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
     return rec
 
 
-def cpu_baseline(cfg_name: str, reps: int = 20, warm: int = 3, timeout_s: float = 240.0):
+def cpu_baseline(cfg_name: str, reps: int = 40, warm: int = 3, timeout_s: float = 240.0):
     """Run ``cpu_child`` in a child process (fresh OpenMP runtime with the placement variables)."""
     import subprocess
 
@@ -705,7 +710,7 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal: numpy backend, gloo, a 64x32x8 tile per rank (no GPU)")
     ap.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
-    ap.add_argument("--cpu-reps", type=int, default=20, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-reps", type=int, default=40, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-warm", type=int, default=3, help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
