@@ -124,6 +124,7 @@ def tune_fields(
         return lambda: stencil(**a, **params, origin=origin, domain=domain, validate_args=False)
 
     if not names:  # nothing written: nothing to place (and the call changes no field)
+        stencil(**arrays, **params, origin=origin, domain=domain)  # full argument checks once
         report["candidates_ms"] = [_time_call(call_with({}), reps)]
         report["untuned_ms"] = report["tuned_ms"] = report["candidates_ms"][0]
         return dict(arrays), report
@@ -142,6 +143,9 @@ def tune_fields(
         for n in names:
             s[n].copy_(backup[n])
     try:
+        # full argument checks once (shapes, origins, domain against the fields' extents): the
+        # timed launches skip validation, as a cached call does
+        stencil(**arrays, **params, origin=origin, domain=domain)
         times = [_time_call(call_with(s), reps) for s in sets]
     finally:
         for n in names:  # the caller's own arrays keep their contents whatever happens

@@ -74,3 +74,23 @@ def test_aliased_written_field_refused():
     names = list(st.field_info)
     with pytest.raises(ValueError, match="shares memory"):
         placement.tune_written_fields(st, {names[0]: a, names[1]: a[:, :, :]}, domain=(8, 8, 4))
+
+
+@pytest.mark.gpu
+def test_invalid_domain_is_rejected_before_any_timed_launch():
+    """The tuner validates the call once (the timed launches skip validation): a domain larger
+    than the fields raises the ordinary ValueError and leaves the fields untouched."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from gt4py_amd import storage
+
+    case = sc.CASES["copy"]
+    st = gtscript.stencil(backend="gt:mi355x", definition=case.definition, externals=case.externals,
+                          name=f"gpu.{case.name}")
+    a = storage.from_array(np.arange(8 * 8 * 4, dtype=np.float64).reshape(8, 8, 4), backend="gt:mi355x")
+    b = storage.zeros((8, 8, 4), np.float64, backend="gt:mi355x")
+    names = list(st.field_info)
+    with pytest.raises(ValueError):
+        placement.tune_written_fields(st, {names[0]: a, names[1]: b}, origin=(0, 0, 0), domain=(9, 8, 4))
+    assert float(b.abs().sum()) == 0.0
