@@ -625,6 +625,55 @@ def traffic_for(cfg, key):
 
 
 EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv", "hdiff_blocks", "staged")
+C5_CONFIG = "hdiff_f32"  # BASELINE configs[4]: 8192x1024x160 f32 per GPU, J strips, RCCL halo
+
+
+def sharded_leg(cfg, args, rank, world, dev, backend, dist) -> dict:
+    """One more config through the N-rank path after the headline (same ranks, same process
+    group): its own fields, halo exchange and timing (barrier + synchronize around K steps, max
+    over ranks). A rank that cannot set the workload up (e.g. out of memory) makes every rank skip
+    the leg together -- a flag is all-reduced first -- so no rank waits in a collective alone."""
+    import torch
+
+    tdev = dev if str(dist.get_backend()).lower() == "nccl" else "cpu"
+    w, err = None, None
+    try:
+        w = Workload(cfg, args, rank, world, dev, backend, dry_run=args.dry_run)
+    except Exception as e:  # noqa: BLE001 - reported in the line, the headline stays valid
+        err = f"{type(e).__name__}: {e}"[:300]
+    ok = torch.tensor([0 if w is None else 1], device=tdev, dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok[0]) == 0:
+        return {"error": err or "the workload failed on another rank"}
+    steps = args.extra_steps
+    el, km = time_workload(w, steps, 3, dev, dist)
+    t = torch.tensor([el, km or 0.0], device=tdev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el, km = float(t[0]), (float(t[1]) if km is not None else None)
+    ni, nj, nk = w.domain
+    gi, gj = w.global_ij
+    rec = {
+        "workload": f"{w.sname} {ni}x{nj}x{nk} {np.dtype(w.dtype).name} per GPU, "
+                    f"{'J-strips' if w.dec2d is None else f'{w.dec2d.pi}x{w.dec2d.pj} tiles'} of a "
+                    f"{gi}x{gj}x{nk} global domain, RCCL halo {w.h}",
+        "n_gpus": world,
+        "global_domain": [gi, gj, nk],
+        "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 4),
+        "step_ms": round(km, 4) if km is not None else None,
+        "Mcells_s": round(gi * gj * nk * steps / el / 1e6, 1),
+        "scaling": "weak",
+        "note": "whole-job cells/s over all ranks (max-over-ranks time); the N=1 line's extra_configs entry "
+                "of this config is the single-GPU reference for weak-scaling efficiency",
+    }
+    if w.placement is not None:
+        rec["placement_untuned_ms"] = w.placement["untuned_ms"]
+        rec["placement_tuned_ms"] = w.placement["tuned_ms"]
+    del w
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return rec
 
 
 # ------------------------------------------------------------------------------------------
@@ -920,6 +969,9 @@ def main():
         result["dry_run"] = True
         result["data"] = "synthetic; DRY RUN on CPU (numpy backend, gloo): not a measurement"
     del wl
+    if world > 1 and not args.no_extra and args.config != C5_CONFIG:
+        # BASELINE configs[4] (C5) at N>1: the f32 tile sharded the same way, in the same ranks
+        result["extra_configs"] = {C5_CONFIG: sharded_leg(C5_CONFIG, args, rank, world, dev, backend, dist)}
     if world == 1 and not args.dry_run and not args.no_extra and not args.halo_selfcomm:
         # the other BASELINE configs, timed in the same process after the headline (C2, C4, the C5
         # per-GPU tile, copy, vadv): per-launch kernel time from HIP events, fraction of 8 TB/s

@@ -45,6 +45,11 @@ def test_bench_launcher_dry_run(gpus, decomp):
         assert isinstance(d["exchange_overhead"], float)
         assert rec["roofline"]["traffic"] is None and "halo step" in rec["roofline"]["traffic_source"]
         assert "step_ms" in rec["roofline"] and "kernel_ms" not in rec["roofline"]
+        # C5 (the f32 tile) through the same N-rank path, whole-job cells/s
+        c5 = rec["extra_configs"]["hdiff_f32"]
+        assert "error" not in c5, c5
+        assert c5["n_gpus"] == gpus and c5["global_domain"][1] == 32 * gpus
+        assert c5["Mcells_s"] > 0 and c5["scaling"] == "weak"
     else:
         assert "dist" not in rec
     for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "roofline", "config"):
