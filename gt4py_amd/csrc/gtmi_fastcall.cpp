@@ -10,7 +10,8 @@
 //     prepared(fields: tuple, params: tuple) -> bool
 //
 // checks that every field argument is still the tensor the entry was made for (same object via
-// its weak reference, same data pointer, same sizes), stores the scalar parameters with the
+// its weak reference, same data pointer, sizes, strides and dtype -- a tensor re-strided in place by
+// transpose_/as_strided_ keeps its identity, pointer and sizes), stores the scalar parameters with the
 // ordinary path's conversions, reads the caller's current HIP stream from c10 and launches.
 // Parameter values are not re-validated, as in the reference, whose _validate_args runs only
 // when the (shapes, origins, parameter names, domain) cache misses (stencil_object.py:578-591).
@@ -48,6 +49,8 @@ struct Check {
     PyObject* wr;  // weak reference to the tensor (owned)
     const void* ptr;
     std::vector<int64_t> sizes;
+    std::vector<int64_t> strides;
+    c10::ScalarType dtype;
 };
 
 struct Prepared {
@@ -120,6 +123,10 @@ PyObject* prepared_call(PyObject* self_, PyObject* args, PyObject* kwargs) {
         c10::IntArrayRef sz = t.sizes();
         if (sz.size() != checks[i].sizes.size() ||
             std::memcmp(sz.data(), checks[i].sizes.data(), sz.size() * sizeof(int64_t)) != 0)
+            Py_RETURN_FALSE;
+        c10::IntArrayRef st = t.strides();  // same rank as the sizes
+        if (std::memcmp(st.data(), checks[i].strides.data(), st.size() * sizeof(int64_t)) != 0 ||
+            t.scalar_type() != checks[i].dtype)
             Py_RETURN_FALSE;
     }
     if ((int)c10::hip::current_device() != self->device) Py_RETURN_FALSE;
@@ -213,6 +220,8 @@ PyObject* prepared_new(PyTypeObject* type, PyObject* args, PyObject* kwargs) {
         const at::Tensor& tt = THPVariable_Unpack(t);
         c.ptr = tt.data_ptr();
         c.sizes.assign(tt.sizes().begin(), tt.sizes().end());
+        c.strides.assign(tt.strides().begin(), tt.strides().end());
+        c.dtype = tt.scalar_type();
         self->checks->push_back(std::move(c));
     }
     return (PyObject*)self;
@@ -245,6 +254,6 @@ PyMODINIT_FUNC PyInit__gtmi_fastcall(void) {
         Py_DECREF(m);
         return nullptr;
     }
-    PyModule_AddIntConstant(m, "ABI", 1);
+    PyModule_AddIntConstant(m, "ABI", 2);
     return m;
 }

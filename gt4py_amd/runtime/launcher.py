@@ -208,7 +208,8 @@ class StencilLauncher:
         ``tensors``: the field arguments in call order (plain torch tensors). Returns
         ``launch(fields, params) -> bool`` -- ``fields`` the field arguments of a call in the same
         order, ``params`` its scalar values in ``param_names`` order -- which launches and returns
-        True when every field is still the same tensor (same object, data pointer and sizes) and
+        True when every field is still the same tensor (same object, data pointer, sizes, strides and
+        dtype) and
         the current device is the arrays' one, else returns False (take the ordinary path); or
         None when this call cannot be prepared. Everything a call does not change (the packed
         ``gtmi_field`` array, the domain, the scalar slots, the foreign function) is built here
@@ -252,14 +253,17 @@ class StencilLauncher:
         raw_stream = torch._C._cuda_getCurrentRawStream
         current_device = torch._C._cuda_getDevice
         slots = [(scalars[j], pos, *ffi.SCALAR_SLOTS[dt]) for pos, j, dt in setters]
-        checks = [(weakref.ref(t), t.data_ptr(), t.shape) for t in tensors]
+        # strides and dtype too: transpose_/as_strided_ re-stride a tensor in place and keep its
+        # identity, data pointer and sizes
+        checks = [(weakref.ref(t), t.data_ptr(), t.shape, t.stride(), t.dtype) for t in tensors]
         n_params = len(param_names)
 
         def launch(fields_now, params) -> bool:
             if len(fields_now) != len(checks) or len(params) != n_params:
                 return False
-            for a, (ref, ptr, shape) in zip(fields_now, checks):
-                if ref() is not a or a.data_ptr() != ptr or a.shape != shape:
+            for a, (ref, ptr, shape, stride, dtype) in zip(fields_now, checks):
+                if (ref() is not a or a.data_ptr() != ptr or a.shape != shape or a.stride() != stride
+                        or a.dtype != dtype):
                     return False
             if current_device() != idx:
                 return False

@@ -93,6 +93,7 @@ def _nt_le(a, b) -> bool:
 # reference's ``_domain_origin_cache`` does (stencil_object.py:579-593).
 
 _FAST_MEMO_MAX = 64
+_FAST_SIGS_PER_ARGS = 8
 
 
 def _plain_value(v) -> bool:
@@ -540,7 +541,12 @@ class StencilObject(abc.ABC):
 
         if len(memo) >= _FAST_MEMO_MAX:
             memo.clear()
-        memo[tuple(id(a) for a in tensors)] = (copy.deepcopy(user_domain), copy.deepcopy(user_origin), launch)
+        # a few (domain, origin) signatures per argument tuple, most recent first: callers that
+        # alternate domains/origins on the same arrays (row bands, boundary regions) keep hitting
+        key = tuple(id(a) for a in tensors)
+        entries = [e for e in memo.get(key, ()) if not (e[0] == user_domain and e[1] == user_origin)]
+        entries.insert(0, (copy.deepcopy(user_domain), copy.deepcopy(user_origin), launch))
+        memo[key] = entries[:_FAST_SIGS_PER_ARGS]
 
     def _run_rows(self, domain, origin, exec_info, arrays, parameter_args, j_split, j_skip):
         ni, nj, nk = domain
@@ -642,16 +648,17 @@ def make_stencil_class(
     parts += ["domain=None", "origin=None", "validate_args=True", "exec_info=None"]
     fdict = ", ".join(f"{n}={n}" for n in field_names)
     pdict = ", ".join(f"{n}={n}" for n in param_names)
-    # fast path (see _fast_tensors): entry = (domain, origin, prepared launch(fields, params) -> bool)
+    # fast path (see _fast_tensors): id tuple -> [(domain, origin, prepared launch(fields, params) -> bool)]
     memo: Dict[tuple, tuple] = {}
     ns["_memo"] = memo
     src = (
         f"def __call__(self, {', '.join(parts)}):\n"
         f"    if exec_info is None:\n"
-        f"        _gt_e = _memo.get({_ids_src(field_names)})\n"
-        f"        if _gt_e is not None and _gt_e[0] == domain and _gt_e[1] == origin and "
-        f"_gt_e[2]({_tuple_src(field_names)}, {_tuple_src(param_names)}):\n"
-        f"            return\n"
+        f"        for _gt_e in _memo.get({_ids_src(field_names)}, ()):\n"
+        f"            if _gt_e[0] == domain and _gt_e[1] == origin:\n"
+        f"                if _gt_e[2]({_tuple_src(field_names)}, {_tuple_src(param_names)}):\n"
+        f"                    return\n"
+        f"                break\n"
         f"    self._call_impl(dict({fdict}), dict({pdict}), domain, origin, validate_args, exec_info)\n"
     )
     exec(compile(src, f"<gt4py_amd:{class_name}.__call__>", "exec"), ns)  # noqa: S102 - generated code

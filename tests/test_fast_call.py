@@ -124,6 +124,93 @@ def test_set_and_resize_take_the_ordinary_path():
     torch.cuda.synchronize()
 
 
+def _square(seed, n=12, nk=4):
+    rng = np.random.default_rng(seed)
+    a = gt_storage.from_array(rng.uniform(-1, 1, (n, n, nk)), backend=BK, aligned_index=(0, 0, 0))
+    b = gt_storage.from_array(rng.uniform(-1, 1, (n, n, nk)), backend=BK, aligned_index=(0, 0, 0))
+    return a, b
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
+@pytest.mark.parametrize("which", ["a", "b", "both"])
+def test_restride_in_place_takes_the_ordinary_path(which):
+    """``transpose_`` on a square-IJ field keeps the tensor's identity, data pointer and sizes but
+    swaps its strides: a prepared launch with the strides packed at bind time would read (or
+    write) the wrong cells, so the entry must miss and the ordinary path re-pack the field."""
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    a, b = _square(21)
+    n, nk = a.shape[0], a.shape[2]
+    dom = (n - 1, n, nk)
+    st(a, b, w=1.25, domain=dom, origin=(0, 0, 0))
+    st(a, b, w=1.25, domain=dom, origin=(0, 0, 0))  # prepared
+    ptrs = (a.data_ptr(), b.data_ptr())
+    for t in ((a,) if which == "a" else (b,) if which == "b" else (a, b)):
+        t.transpose_(0, 1)
+    assert (a.data_ptr(), b.data_ptr()) == ptrs and a.shape == b.shape == (n, n, nk)
+    want = _expect(a, 1.25, dom, b_init=gt_storage.to_numpy(b))
+    st(a, b, w=1.25, domain=dom, origin=(0, 0, 0))
+    np.testing.assert_array_equal(gt_storage.to_numpy(b), want)
+    want = _expect(a, -0.5, dom, b_init=gt_storage.to_numpy(b))
+    st(a, b, w=-0.5, domain=dom, origin=(0, 0, 0))  # the re-made entry hits
+    np.testing.assert_array_equal(gt_storage.to_numpy(b), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
+def test_as_strided_in_place_takes_the_ordinary_path():
+    """``as_strided_`` to a new I stride (every other row of a larger buffer) with the same
+    sizes and storage offset, on the call and the frozen path."""
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    rng = np.random.default_rng(22)
+    n, nj, nk = 9, 7, 3
+    a = gt_storage.from_array(rng.uniform(-1, 1, (2 * n + 2, nj, nk)), backend=BK, aligned_index=(0, 0, 0))
+    b = gt_storage.zeros((n, nj, nk), np.float64, backend=BK)
+    dom = (n, nj, nk)
+    a_big = gt_storage.to_numpy(a).copy()
+    a.as_strided_((n + 1, nj, nk), a.stride(), a.storage_offset())
+    fz = st.freeze(origin={"a": (0, 0, 0), "b": (0, 0, 0)}, domain=dom)
+    for call in (lambda w: st(a, b, w=w, domain=dom, origin=(0, 0, 0)), lambda w: fz(a=a, b=b, w=w)):
+        call(2.0)
+        call(2.0)  # prepared
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a_big[:n + 1], 2.0, dom, b_init=np.zeros(dom)))
+        s0, s1, s2 = a.stride()
+        a.as_strided_((n + 1, nj, nk), (2 * s0, s1, s2), a.storage_offset())
+        call(2.0)
+        np.testing.assert_array_equal(gt_storage.to_numpy(b), _expect(a_big[0::2], 2.0, dom, b_init=np.zeros(dom)))
+        a.as_strided_((n + 1, nj, nk), (s0, s1, s2), a.storage_offset())
+        b.zero_()
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("mode")
+def test_alternating_domains_keep_their_entries():
+    """Two (domain, origin) signatures on the same arrays both stay prepared (advisor r03: a
+    single entry per argument tuple re-bound on every alternation)."""
+    _need_gpu()
+    st = gtscript.stencil(backend=BK, definition=shift_axpy, name="fast_call.axpy")
+    st.clean_call_args_cache()
+    a, b = _fields(23)
+    sigs = [((17, 4, 5), {"a": (0, 0, 0), "b": (0, 0, 0)}), ((17, 5, 5), {"a": (0, 4, 0), "b": (0, 4, 0)})]
+    for it in range(6):
+        dom, org = sigs[it % 2]
+        b.zero_()
+        st(a, b, w=0.5 + it, domain=dom, origin=org)
+        np.testing.assert_array_equal(gt_storage.to_numpy(b),
+                                      _expect(a, 0.5 + it, dom, org["a"], org["b"], b_init=np.zeros((17, 9, 5))))
+    (entries,) = _memo(st).values()
+    assert len(entries) == 2
+    launches = [e[2] for e in entries]
+    for it in range(4):
+        dom, org = sigs[it % 2]
+        st(a, b, w=1.0, domain=dom, origin=org)
+    assert [e[2] for e in _memo(st)[next(iter(_memo(st)))]] in (launches, launches[::-1])
+
+
 @pytest.mark.gpu
 @pytest.mark.usefixtures("mode")
 def test_domain_and_origin_changes():
@@ -199,7 +286,8 @@ def test_parameter_types_and_entry_kind(mode):
         with pytest.raises(TypeError):
             st(a, b, w=bad, domain=dom, origin=(0, 0, 0))
     st(a, b, w=0.5, domain=dom, origin=(0, 0, 0))
-    (entry,) = _memo(st).values()
+    (entries,) = _memo(st).values()
+    (entry,) = entries
     assert (type(entry[2]).__name__ == "Prepared") == (mode == "native")
     for w in (np.float32(1.5), 2, np.float64(-0.25), np.int64(3), True, 0.125):
         st(a, b, w=w, domain=dom, origin=(0, 0, 0))
@@ -233,6 +321,9 @@ def test_native_prepared_rejects_other_arguments():
     assert p((x,), (1.0,)) is False  # too few fields
     assert p((x, y), ()) is False  # too few params
     assert p([x, y], (1.0,)) is False  # not a tuple
+    x.as_strided_((4, 3, 2), (1, 4, 12))
+    assert p((x, y), (1.0,)) is False  # same object, data pointer and sizes; new strides
+    x.as_strided_((4, 3, 2), (6, 2, 1))
     y.set_(torch.zeros(4, 3, 2).untyped_storage())
     assert p((x, y), (1.0,)) is False  # same object, new data
     with pytest.raises(TypeError):
