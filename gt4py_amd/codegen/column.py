@@ -161,6 +161,25 @@ class ColumnGen:
             conds.insert(0, "alive")
         return " && ".join(conds) if conds else None
 
+    def _tile_local(self, li, si, ti) -> Optional[str]:
+        """Tile mode: the lanes of the block on which top-level statement ti is valid -- the owned
+        tile grown by the statement's own extent. Outside it a statement's cross-column reads
+        reach past the tile (e.g. ``[tx-1]`` at tx = 0), so a halo lane that still passes the
+        global ``_guard`` computes garbage; a store of that garbage to a scratch field would race
+        with the tile that owns the column. Extent analysis makes every producer
+        valid wherever its consumers are, so the guard never starves a valid lane."""
+        (a, b), (c, d) = self.a.extents.blocks.get((li, si, ti), ((0, 0), (0, 0)))
+        eilo, _, ejlo, _ = self.ext
+        TI, TJ = self._tile_geom()
+        conds = []
+        if a < eilo:
+            conds.append(f"tx >= {eilo - a}")
+        conds.append(f"tx < {eilo + TI + b}")
+        if c < ejlo:
+            conds.append(f"ty >= {ejlo - c}")
+        conds.append(f"ty < {ejlo + TJ + d}")
+        return " && ".join(conds)
+
     # ------------------------------------------------------------------ analysis
     def _analyse_loop(self, li) -> _LoopInfo:
         vl = self.st.vertical_loops[li]
@@ -656,6 +675,9 @@ class ColumnGen:
                             pending.clear()
                     code = self._stmt(s, rend, wvar, mem_store)
                     g = self._guard(li, si, ti)
+                    if self.tile and any(w and self._mem(a.name) and a.name not in self.api
+                                         for a, w in iter_accesses([s])):
+                        g = f"{g} && {self._tile_local(li, si, ti)}" if g else self._tile_local(li, si, ti)
                     if g:
                         code = [f"if ({g}) {{"] + ["    " + x for x in code] + ["}"]
                     body += code

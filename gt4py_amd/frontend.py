@@ -132,6 +132,10 @@ class StencilParser:
         self.api_order: List[str] = []
         self._uid = itertools.count()
         self.used_externals: Dict[str, Any] = {}
+        # names assigned so far outside horizontal regions (reference IRMaker.written_vars,
+        # gtscript_frontend.py:920, 1891-1892)
+        self.written_vars: set = set()
+        self._in_region = 0
 
     # ------------------------------------------------------------------ signature
     def _parse_signature(self):
@@ -432,11 +436,29 @@ class StencilParser:
         if isinstance(s, ast.With):
             name = self._call_name(s.items[0].context_expr)
             if name == "horizontal":
+                where = (f"Invalid 'with' statement in '{self.definition.__name__}' at line {s.lineno} "
+                         f"(column {s.col_offset + 1})")
+                if any(isinstance(c, ast.With) for c in s.body):
+                    raise GTScriptSyntaxError(f"{where}: Cannot nest `with` node inside a horizontal region.")
                 masks = []
                 for item in s.items:
                     for reg in item.context_expr.args:
                         masks.append(self._parse_region(reg, scope))
-                return [ir.HorizontalRegion(masks, self._parse_block(s.body, scope))]
+                self._in_region += 1
+                try:
+                    body = self._parse_block(s.body, scope)
+                finally:
+                    self._in_region -= 1
+                # a value written earlier and read at an IJ offset inside a region: the reference
+                # refuses it (gtscript_frontend.py:1952-1956)
+                offs = {a.name for n in body for a in ir.walk(n)
+                        if isinstance(a, ir.FieldAccess) and (a.offset[0] != 0 or a.offset[1] != 0)}
+                bad = sorted(offs & self.written_vars)
+                if bad:
+                    raise GTScriptSyntaxError(
+                        f"{where} The following variables are written before being referenced with an offset in "
+                        f"a horizontal region: {', '.join(bad)}")
+                return [ir.HorizontalRegion(masks, body)]
             raise GTScriptSyntaxError(f"Invalid 'with' statement inside a computation (line {s.lineno})")
         if isinstance(s, ast.Return):
             raise GTScriptSyntaxError("'return' is only allowed in gtscript functions")
@@ -657,6 +679,8 @@ class StencilParser:
                     raise GTScriptSyntaxError("Assignment with a K offset is only supported for API fields")
         else:
             tgt = ir.FieldAccess(name_res, (0, 0, 0))
+        if not self._in_region:
+            self.written_vars.add(name_res)
         return pre + [ir.Assign(tgt, val)]
 
     # ------------------------------------------------------------------ expressions

@@ -63,6 +63,15 @@ def _np_dtype_of(t) -> np.dtype:
 _SCALAR_KIND = {"float64": 0, "float32": 1, "int64": 2, "int32": 3, "int16": 4, "int8": 5, "bool": 6}
 
 
+_LAUNCHERS = weakref.WeakSet()
+
+
+def drop_pack_caches() -> None:
+    """Forget the packed argument arrays of every launcher (see ``drop_prepared_launches``)."""
+    for la in list(_LAUNCHERS):
+        la._pack_cache.clear()
+
+
 class StencilLauncher:
     def __init__(self, lib_path: str, name: str = ""):
         self.lib_path = lib_path
@@ -70,6 +79,7 @@ class StencilLauncher:
         self._lib = None
         self._scratch_cache: Dict[Tuple, Any] = {}
         self._pack_cache: Dict[Tuple, Any] = {}
+        _LAUNCHERS.add(self)
 
     @property
     def lib(self) -> ffi.StencilLibrary:

@@ -95,6 +95,33 @@ def _nt_le(a, b) -> bool:
 _FAST_MEMO_MAX = 64
 _FAST_SIGS_PER_ARGS = 8
 
+# every prepared-launch memo (per StencilObject class, per FrozenStencil): they hold weak
+# references to the argument tensors (drop_prepared_launches)
+_CLASS_MEMOS: list = []
+_FROZEN = None  # id -> FrozenStencil (weak values; frozen stencils are not hashable), made on first use
+
+
+def _frozen_set():
+    global _FROZEN
+    if _FROZEN is None:
+        import weakref
+
+        _FROZEN = weakref.WeakValueDictionary()
+    return _FROZEN
+
+
+def drop_prepared_launches() -> None:
+    """Forget every prepared launch and packed argument array (they hold weak references to and
+    borrowed pointers of the argument tensors): the next call of each signature prepares it
+    again. Used before tensors are re-homed in place (``storage.placement.tune_in_place``)."""
+    for memo in _CLASS_MEMOS:
+        memo.clear()
+    for fz in list(_frozen_set().values()):
+        fz._memo.clear()
+    from gt4py_amd.runtime.launcher import drop_pack_caches
+
+    drop_pack_caches()
+
 
 def _plain_value(v) -> bool:
     """A domain / origin value the fast path may compare with ``==`` (ints, tuples, dicts)."""
@@ -164,6 +191,20 @@ class FrozenStencil:
         exec(compile(src, "<gt4py_amd:FrozenStencil._fast>", "exec"), ns)  # noqa: S102 - generated code
         object.__setattr__(self, "_memo", memo)
         object.__setattr__(self, "_fast", ns["_fast"])
+        _frozen_set()[id(self)] = self
+
+    def tune_placement(self, *, candidates: int = 3, reps: int = 10, **kwargs) -> Dict[str, Any]:
+        """Re-home the fields this stencil writes, in place, to the fastest of ``candidates + 1``
+        HBM buffer sets for this frozen domain/origin (``storage.placement.tune_in_place``):
+        takes the keyword arguments of a call; the tensors stay the same objects. Returns the
+        report (every set's kernel time, set 0 = the current allocation)."""
+        from gt4py_amd.storage.placement import tune_in_place
+
+        so = self.stencil_object
+        fields = {n: kwargs[n] for n in so.field_info}
+        params = {n: kwargs[n] for n in so.parameter_info if n in kwargs}
+        return tune_in_place(so, fields, origin=self.origin, domain=self.domain, params=params,
+                             candidates=candidates, reps=reps)
 
     def __call__(self, **kwargs) -> None:
         if self._fast(kwargs):  # exactly the field and parameter arguments, a prepared launch
@@ -581,6 +622,25 @@ class StencilObject(abc.ABC):
             type.__setattr__(type(self), "_gt_frozen_cls_", cls)
         return cls(self, origin, domain)
 
+    def tune_placement(self, *args, candidates: int = 3, reps: int = 10, origin=None, domain=None,
+                       **kwargs) -> Dict[str, Any]:
+        """Opt-in HBM placement for the drop-in path (DESIGN.md §5 "HBM placement"): called with
+        the arguments of an ordinary call, it re-homes the fields the stencil writes IN PLACE to
+        the fastest of ``candidates + 1`` buffer sets (``storage.placement.tune_in_place``) --
+        the caller's tensors stay the same objects with the same contents, on other pages. Once,
+        after allocating the fields; returns the report (every set's kernel time in ms, set 0 =
+        the current allocation)."""
+        import inspect
+
+        from gt4py_amd.storage.placement import tune_in_place
+
+        bound = inspect.signature(self.definition_func).bind(*args, **kwargs)
+        bound.apply_defaults()
+        fields = {n: v for n, v in bound.arguments.items() if n in self.field_info}
+        params = {n: v for n, v in bound.arguments.items() if n in self.parameter_info}
+        return tune_in_place(self, fields, origin=origin, domain=domain, params=params, candidates=candidates,
+                             reps=reps)
+
     def clean_call_args_cache(self) -> None:
         type(self)._domain_origin_cache.clear()
         memo = type(self).__dict__.get("_gt_fast_memo_")
@@ -650,6 +710,7 @@ def make_stencil_class(
     pdict = ", ".join(f"{n}={n}" for n in param_names)
     # fast path (see _fast_tensors): id tuple -> [(domain, origin, prepared launch(fields, params) -> bool)]
     memo: Dict[tuple, tuple] = {}
+    _CLASS_MEMOS.append(memo)
     ns["_memo"] = memo
     src = (
         f"def __call__(self, {', '.join(parts)}):\n"

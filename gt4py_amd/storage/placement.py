@@ -19,6 +19,12 @@ fields in the fastest set, holding the contents they had before (restored from a
 timing launches write them; the caller's original arrays are restored too, also when a call
 raises). The report lists every set's time; the unchosen buffers are freed.
 
+Drop-in form: ``stencil.tune_placement(*args, origin=..., domain=..., candidates=3, **params)`` (and
+``FrozenStencil.tune_placement(**kwargs)``) takes the arguments of an ordinary call and re-homes
+the written fields IN PLACE (:func:`tune_in_place`): the caller's tensor objects stay the same and
+now live on the chosen buffers, so a reference-API user opts in with one line and re-plumbs
+nothing.
+
 The reference has no counterpart: its storages are plain CuPy/NumPy allocations
 (``/root/reference/src/gt4py/storage/cartesian/interface.py:143-327``); this tool only returns
 other allocations of the same layout, so everything downstream sees ordinary fields.
@@ -168,3 +174,79 @@ def like_bytes(t) -> int:
     """Bytes a :func:`like` copy of ``t`` allocates."""
     span = 1 + sum((s - 1) * st for s, st in zip(t.shape, t.stride())) if t.numel() else 0
     return span * t.element_size() + _RESIDUE
+
+
+def _storage_refs(t) -> Optional[int]:
+    use = getattr(__import__("torch")._C, "_storage_Use_Count", None)
+    if use is None:
+        return None
+    st = t.untyped_storage()
+    return int(use(st._cdata)) - 1  # minus the temporary storage object itself
+
+
+def _exclusive(t) -> bool:
+    """``t`` is the only tensor on its storage (besides the flat buffer a gt4py_amd storage is a
+    strided view of): re-homing it cannot leave another view writing the old pages."""
+    import sys
+
+    refs = _storage_refs(t)
+    if refs is None:  # no use count in this torch: accept only tensors that are not views
+        return t._base is None
+    if t._base is None:
+        return refs <= 1
+    # a view: only of a flat buffer nothing else holds (getrefcount: the view's own reference
+    # plus the call's argument)
+    return refs <= 2 and t._base._base is None and sys.getrefcount(t._base) <= 2
+
+
+def tune_in_place(
+    stencil,
+    arrays: Dict[str, Any],
+    *,
+    origin=None,
+    domain=None,
+    params: Optional[Dict[str, Any]] = None,
+    candidates: int = 3,
+    reps: int = 10,
+    memory_fraction: float = 0.8,
+) -> Dict[str, Any]:
+    """:func:`tune_written_fields`, then move each written field the tuner re-homed into the
+    CALLER'S tensor object (``torch.utils.swap_tensors``): same object, same sizes, strides,
+    dtype and contents, new buffer; the old buffer is freed. Returns the report (with
+    ``"in_place": True``).
+
+    Raises ``ValueError`` (before anything is timed) for a written field that other tensors view
+    (they would keep the old pages) and ``RuntimeError`` if a field is weakly referenced outside
+    gt4py_amd; gt4py_amd's own prepared launches and packed-argument caches are dropped first
+    (they hold weak references and borrowed pointers; the next call re-prepares them).
+    """
+    import torch
+
+    names = written_fields(stencil)
+    for n in names:
+        t = arrays.get(n)
+        if not (type(t) is torch.Tensor and t.is_cuda):
+            raise TypeError(f"tune_placement: '{n}' is not a plain device torch.Tensor")
+        if not _exclusive(t):
+            raise ValueError(f"tune_placement: written field '{n}' shares its storage with other tensors "
+                             f"(views would keep the old buffer); use tune_written_fields and pass the returned arrays")
+    out, report = tune_written_fields(stencil, arrays, origin=origin, domain=domain, params=params,
+                                      candidates=candidates, reps=reps, memory_fraction=memory_fraction)
+    moved = [n for n in names if out[n] is not arrays[n]]
+    if moved:
+        import weakref
+
+        from gt4py_amd.stencil_object import drop_prepared_launches
+
+        drop_prepared_launches()
+        held = [n for n in moved if weakref.getweakrefcount(arrays[n])]
+        if held:
+            raise RuntimeError(f"tune_placement: field(s) {held} are weakly referenced elsewhere; cannot re-home "
+                               "them in place (use tune_written_fields)")
+        for n in moved:
+            torch.utils.swap_tensors(arrays[n], out[n])  # arrays[n] now holds the chosen buffer
+        del out
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    report["in_place"] = True
+    return report

@@ -89,8 +89,11 @@ def generate(seed):
             if v2 and r.random() < 0.6:
                 ib = r.choice(("region[I[0] : I[0] + 2, :]", "region[:, J[-1] - 1 : J[-1]]",
                                "region[I[0] : I[0] + 3, J[0] : J[0] + 2]", "region[I[-1] - 2 : I[-1], :]"))
+                # no temporaries inside the region: a value written before and read at an IJ
+                # offset in a horizontal region is refused by the reference frontend
+                # (gtscript_frontend.py:1952-1956), and at offset 0 they add nothing new
                 L.append(f"        with horizontal({ib}):")
-                L.append(f"            out1 = {g.expr(2, 'offsets', kmode)} + out1")
+                L.append(f"            out1 = {g.expr(2, False, kmode)} + out1")
             if v2:
                 g.prev_temps = list(g.temps)  # readable (at IJ offsets) by a later sequential sweep
             g.temps = []  # temporaries are local to the computation
@@ -124,3 +127,32 @@ def generate(seed):
         L.append("    with computation(PARALLEL), interval(...):")
         L.append("        out1 = a")
     return "\n".join(L) + "\n", name
+
+
+# seeds whose programs take the tile-kernel path (checked by tests/test_tile.py::
+# test_fuzz_golden_programs_take_the_tile_path); their sources are committed as
+# tests/fuzz_golden_programs.py and pinned to reference-generated goldens (stencil_cases.py)
+GOLDEN_SEEDS = [1003, 1005, 1011, 1014, 1029, 1045, 1057, 5001, 5002, 5010, 5069, 5089]
+
+
+def emit(seeds) -> str:
+    """The source of a module defining ``fuzz_<seed>`` for every seed (``SEEDS`` lists them)."""
+    out = ['"""Generated by ``python tests/fuzz_stencils.py`` from tests/fuzz_stencils.py (do not edit):',
+           "differential-fuzz programs that take the tile-kernel path, pinned to reference goldens",
+           '(tests/stencil_cases.py, fuzz_tile_<seed>)."""', "",
+           "import numpy as np",
+           "from gt4py_amd.gtscript import BACKWARD, FORWARD, PARALLEL, Field, I, J, computation, horizontal, "
+           "interval, region  # noqa: F401", "", f"SEEDS = {list(seeds)!r}", ""]
+    for seed in seeds:
+        src, _ = generate(seed)
+        out += ["", src]
+    return "\n".join(out).rstrip("\n") + "\n"
+
+
+if __name__ == "__main__":
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fuzz_golden_programs.py")
+    with open(path, "w") as f:
+        f.write(emit(GOLDEN_SEEDS))
+    print(path)

@@ -2138,3 +2138,143 @@ def tail_bwd_fwd(a: F64, c: F64, out: F64):
 
 case("tail_bwd_fwd", fields={"a": fs(6, 5, 130), "c": fs(6, 5, 130), "out": fs(6, 5, 130, init="zeros")})(tail_bwd_fwd)
 case("tail_bwd_fwd_short", fields={"a": fs(6, 5, 9), "c": fs(6, 5, 9), "out": fs(6, 5, 9, init="zeros")})(tail_bwd_fwd)
+
+
+# --------------------------------------------------------------------------------------
+# Tile kernels (column kernels in tile mode, codegen/column.py): sequential sweeps that read
+# their own products across columns -- the reference's IJ caches
+# (gtc/passes/oir_optimizations/caches.py:44-90). Ragged domains leave partial tiles on both
+# axes (the default f64 tile is 48 x 6 outputs, f32 112 x 6).
+# --------------------------------------------------------------------------------------
+
+
+def bwd_recurrence_ij_temp(a: F64, b: F64, out: F64):
+    with computation(BACKWARD):
+        with interval(-1, None):
+            s = a
+        with interval(0, -1):
+            s = s[0, 0, 1] * 0.25 + a - b
+    with computation(BACKWARD), interval(...):
+        t = s * b
+        out = t[0, -1, 0] + t[0, 1, 0] - 2.0 * t[-2, 0, 0] + t[2, 0, 0]
+
+
+def two_phase_chain(a: F64, c: F64, out: F64):
+    with computation(FORWARD), interval(...):
+        t1 = a * c + 1.0
+        t2 = t1[1, 0, 0] + t1[-1, 0, 0] - t1
+        out = t2[0, 1, 0] - t2[0, -1, 0] + c
+
+
+def tile_with_k_window(a: F64, w: F64, out: F64):
+    with computation(FORWARD):
+        with interval(0, 1):
+            acc = a
+        with interval(1, None):
+            acc = acc[0, 0, -1] + a * w
+    with computation(FORWARD):
+        with interval(0, 1):
+            t0 = acc * w
+            out = t0[1, 0, 0] - t0[0, -1, 0]
+        with interval(1, None):
+            t1 = acc + w * acc[0, 0, -1]
+            out = t1[1, 0, 0] - t1[0, -1, 0] + out[0, 0, -1] * 0.5
+
+
+def tile_conditional(a: F64, out: F64):
+    with computation(FORWARD):
+        with interval(0, 1):
+            m = a
+        with interval(1, None):
+            m = m[0, 0, -1] if m[0, 0, -1] > a else a
+    with computation(FORWARD), interval(...):
+        d = m - a
+        if d[1, 0, 0] > d[-1, 0, 0]:
+            out = d[1, 0, 0] + d[0, 1, 0]
+        else:
+            out = d[-1, 0, 0] - d[0, -1, 0]
+
+
+def tile_f32(a: F32, out: F32):
+    with computation(FORWARD):
+        with interval(0, 1):
+            s = a
+        with interval(1, None):
+            s = s[0, 0, -1] * 0.5 + a
+    with computation(FORWARD), interval(...):
+        t = s * 3.0
+        out = t[1, 1, 0] - t[-1, -1, 0]
+
+
+
+def tile_scratch_product(a: F64, out: F64):
+    """A tile-kernel temporary (t2, read across columns through u's LDS plane) that a later
+    PARALLEL kernel reads at IJ offsets, so it is stored to a scratch field from the tile kernel:
+    only lanes on which t2 is valid may store it (codegen/column.py _tile_local)."""
+    with computation(FORWARD):
+        with interval(0, 1):
+            t1 = a * 0.5
+        with interval(1, None):
+            t1 = t1[0, 0, -1] * 0.5 + a
+    with computation(FORWARD), interval(...):
+        u = t1 * 2.0 + a
+        t2 = u[1, 0, 0] - u[-1, 0, 0] + u[0, 1, 0]
+    with computation(PARALLEL), interval(...):
+        out = t2[1, 0, 0] + t2[-1, 0, 0] - t2[0, -1, 0]
+
+
+# name: (definition, {field: (halo_i_lo, halo_i_hi, halo_j_lo, halo_j_hi)}, dtype)
+TILE_PROGRAMS = {
+    "fwd_recurrence_ij_temp": (staged_forward_ij_temp, {"a": (1, 1, 0, 1)}, "f8"),
+    "bwd_recurrence_ij_temp": (bwd_recurrence_ij_temp, {"a": (2, 2, 1, 1), "b": (2, 2, 1, 1)}, "f8"),
+    "two_phase_chain": (two_phase_chain, {"a": (1, 1, 1, 1), "c": (1, 1, 1, 1)}, "f8"),
+    "tile_with_k_window": (tile_with_k_window, {"a": (0, 1, 1, 0), "w": (0, 1, 1, 0)}, "f8"),
+    "tile_conditional": (tile_conditional, {"a": (1, 1, 1, 1)}, "f8"),
+    "tile_f32": (tile_f32, {"a": (1, 1, 1, 1)}, "f4"),
+    "tile_scratch_product": (tile_scratch_product, {"a": (2, 2, 1, 1)}, "f8"),
+}
+TILE_DOMAINS = {"d70": (70, 9, 6), "d131": (131, 23, 13)}
+TILE_GOLDEN = []  # golden case names, one per (program, domain)
+
+
+def _tile_cases():
+    for prog, (defn, halos, dt) in TILE_PROGRAMS.items():
+        for tag, (ni, nj, nk) in TILE_DOMAINS.items():
+            fields, origin = {}, {}
+            for f, (ilo, ihi, jlo, jhi) in halos.items():
+                fields[f] = fs(ni + ilo + ihi, nj + jlo + jhi, nk, dtype=dt, init=("u", 0.5, 2.0))
+                origin[f] = (ilo, jlo, 0)
+            fields["out"] = fs(ni, nj, nk, dtype=dt, init="zeros")
+            origin["out"] = (0, 0, 0)
+            name = f"tile_{prog}_{tag}"
+            case(name, fields=fields, origin=origin, domain=(ni, nj, nk), features=("tile",))(defn)
+            TILE_GOLDEN.append(name)
+
+
+_tile_cases()
+
+
+# --------------------------------------------------------------------------------------
+# Differential-fuzz programs that take the tile path (tests/fuzz_stencils.py seeds; their
+# sources are committed in tests/fuzz_golden_programs.py so the reference frontend can read
+# them), pinned to the reference numpy backend at ragged domains
+# --------------------------------------------------------------------------------------
+
+import fuzz_golden_programs as _fgp  # noqa: E402
+
+FUZZ_GOLDEN = []
+
+
+def _fuzz_cases():
+    for n, seed in enumerate(_fgp.SEEDS):
+        ni, nj, nk = TILE_DOMAINS["d70" if n % 2 == 0 else "d131"]
+        fields = {f: fs(ni + 4, nj + 4, nk, init=("u", -4.0, 4.0)) for f in ("a", "b", "c")}
+        fields.update({f: fs(ni, nj, nk, init=("u", -1.0, 1.0)) for f in ("out1", "out2")})
+        origin = {"a": (2, 2, 0), "b": (2, 2, 0), "c": (2, 2, 0), "out1": (0, 0, 0), "out2": (0, 0, 0)}
+        name = f"fuzz_tile_{seed}"
+        case(name, fields=fields, params={"s": 0.75}, origin=origin, domain=(ni, nj, nk),
+             features=("tile", "fuzz"))(getattr(_fgp, f"fuzz_{seed}"))
+        FUZZ_GOLDEN.append(name)
+
+
+_fuzz_cases()

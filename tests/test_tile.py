@@ -5,8 +5,10 @@ sequential sweeps that read their own products across columns, after
 per level on overlapping 2-D tiles instead of the staged lowering's scratch round trips.
 
 CPU tests check the plans (which stencils take the tile path, which fusions are refused);
-GPU tests compare every stencil with the numpy backend (itself pinned to the reference's
-fixtures), bit for bit, on ragged domains that leave partial tiles on both axes.
+GPU tests compare every program with the reference numpy backend's own outputs (goldens
+``tile_<program>_d70`` / ``_d131`` and ``fuzz_tile_<seed>``, tests/stencil_cases.py, made by
+tests/golden/make_golden.py) under every tile geometry, bit for bit, on ragged domains that
+leave partial tiles on both axes, and with the numpy backend at a tiny domain.
 """
 
 import numpy as np
@@ -19,88 +21,25 @@ F64 = Field[np.float64]
 F32 = Field[np.float32]
 
 
-def fwd_recurrence_ij_temp(a: F64, out: F64):
-    with computation(FORWARD):
-        with interval(0, 1):
-            s = a
-        with interval(1, None):
-            s = s[0, 0, -1] * 0.5 + a
-    with computation(FORWARD), interval(...):
-        t = s * 2.0 + a
-        out = t[1, 0, 0] - t[-1, 0, 0] + t[0, 1, 0] * s
-
-
-def bwd_recurrence_ij_temp(a: F64, b: F64, out: F64):
-    with computation(BACKWARD):
-        with interval(-1, None):
-            s = a
-        with interval(0, -1):
-            s = s[0, 0, 1] * 0.25 + a - b
-    with computation(BACKWARD), interval(...):
-        t = s * b
-        out = t[0, -1, 0] + t[0, 1, 0] - 2.0 * t[-2, 0, 0] + t[2, 0, 0]
-
-
-def two_phase_chain(a: F64, c: F64, out: F64):
-    with computation(FORWARD), interval(...):
-        t1 = a * c + 1.0
-        t2 = t1[1, 0, 0] + t1[-1, 0, 0] - t1
-        out = t2[0, 1, 0] - t2[0, -1, 0] + c
-
-
-def tile_with_k_window(a: F64, w: F64, out: F64):
-    with computation(FORWARD):
-        with interval(0, 1):
-            acc = a
-        with interval(1, None):
-            acc = acc[0, 0, -1] + a * w
-    with computation(FORWARD):
-        with interval(0, 1):
-            t0 = acc * w
-            out = t0[1, 0, 0] - t0[0, -1, 0]
-        with interval(1, None):
-            t1 = acc + w * acc[0, 0, -1]
-            out = t1[1, 0, 0] - t1[0, -1, 0] + out[0, 0, -1] * 0.5
-
-
-def tile_conditional(a: F64, out: F64):
-    with computation(FORWARD):
-        with interval(0, 1):
-            m = a
-        with interval(1, None):
-            m = m[0, 0, -1] if m[0, 0, -1] > a else a
-    with computation(FORWARD), interval(...):
-        d = m - a
-        if d[1, 0, 0] > d[-1, 0, 0]:
-            out = d[1, 0, 0] + d[0, 1, 0]
-        else:
-            out = d[-1, 0, 0] - d[0, -1, 0]
-
-
-def tile_f32(a: F32, out: F32):
-    with computation(FORWARD):
-        with interval(0, 1):
-            s = a
-        with interval(1, None):
-            s = s[0, 0, -1] * 0.5 + a
-    with computation(FORWARD), interval(...):
-        t = s * 3.0
-        out = t[1, 1, 0] - t[-1, -1, 0]
-
+from stencil_cases import (  # noqa: E402  (the programs live with their reference goldens)
+    FUZZ_GOLDEN,
+    TILE_GOLDEN,
+    TILE_PROGRAMS,
+    bwd_recurrence_ij_temp,
+    tile_conditional,
+    tile_f32,
+    tile_scratch_product,
+    tile_with_k_window,
+    two_phase_chain,
+)
+from stencil_cases import staged_forward_ij_temp as fwd_recurrence_ij_temp  # noqa: E402
 
 # (tile_by, tile_ti, tile_bx): block rows, tile width in I and block lanes in I (0: defaults,
 # the aligned tile width and 64 or 128 lanes by cell size)
 GEOMS = [(8, 0, 0), (4, 0, 0), (16, 0, 0), (8, 60, 64), (16, 13, 0), (4, 0, 128), (8, 100, 128)]
 
 # name: (definition, {field: (halo_i_lo, halo_i_hi, halo_j_lo, halo_j_hi)}, dtype)
-CASES = {
-    "fwd_recurrence_ij_temp": (fwd_recurrence_ij_temp, {"a": (1, 1, 0, 1)}, np.float64),
-    "bwd_recurrence_ij_temp": (bwd_recurrence_ij_temp, {"a": (2, 2, 1, 1), "b": (2, 2, 1, 1)}, np.float64),
-    "two_phase_chain": (two_phase_chain, {"a": (1, 1, 1, 1), "c": (1, 1, 1, 1)}, np.float64),
-    "tile_with_k_window": (tile_with_k_window, {"a": (0, 1, 1, 0), "w": (0, 1, 1, 0)}, np.float64),
-    "tile_conditional": (tile_conditional, {"a": (1, 1, 1, 1)}, np.float64),
-    "tile_f32": (tile_f32, {"a": (1, 1, 1, 1)}, np.float32),
-}
+CASES = {name: (defn, halos, np.dtype(dt).type) for name, (defn, halos, dt) in TILE_PROGRAMS.items()}
 
 
 def _stencil(name, backend, **opts):
@@ -110,11 +49,30 @@ def _stencil(name, backend, **opts):
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_tile_plan(name):
-    """Each case fuses into one sweep and runs as a tile kernel (no scratch)."""
+    """Each case fuses into one sweep and runs as a tile kernel (no scratch, except
+    tile_scratch_product, whose tile-kernel product t2 a later kernel reads at IJ offsets)."""
     st = _stencil(name, "gt:mi355x")
     plan = st._gt_run_impl_.compiled.plan
     assert any(getattr(k, "tile", False) for k in plan.kernels), plan
-    assert not plan.scratch, plan
+    assert plan.scratch == (["t2"] if name == "tile_scratch_product" else []), plan
+
+
+@pytest.mark.parametrize("name", FUZZ_GOLDEN)
+def test_fuzz_golden_programs_take_the_tile_path(name):
+    import stencil_cases as sc
+
+    case = sc.CASES[name]
+    st = gtscript.stencil(backend="gt:mi355x", definition=case.definition, name=f"golden.{name}")
+    assert any(getattr(k, "tile", False) for k in st._gt_run_impl_.compiled.plan.kernels)
+
+
+def test_scratch_stores_of_tile_kernels_are_tile_local():
+    """Only lanes on which the stored temporary is valid store it (the owned tile grown by the
+    statement's extent), so overlapping tiles never race on a scratch column."""
+    st = _stencil("tile_scratch_product", "gt:mi355x")
+    src = st._gt_run_impl_.compiled.source
+    store = [ln for ln in src.splitlines() if "if (alive" in ln and "tx <" in ln]
+    assert store, "no tile-local guard in the tile kernel"
 
 
 def test_tile_off_uses_staged_lowering():
@@ -176,11 +134,41 @@ def _inputs(name, domain, seed):
     return arrays, origins
 
 
+# every geometry on the ragged 131 x 23 x 13 domain of each program and on four fuzz programs
+# (every golden also runs with the default geometry in test_gpu_parity.py::test_golden_case)
+GEOM_GOLDEN = [n for n in TILE_GOLDEN if n.endswith("_d131")] + FUZZ_GOLDEN[:4]
+
+
+def geom_opts(geom):
+    tile_by, tile_ti, tile_bx = geom
+    return {"tile_by": tile_by, "tile_ti": tile_ti, "tile_bx": tile_bx}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GEOM_GOLDEN)
+@pytest.mark.parametrize("geom", GEOMS)
+def test_tile_geometries_vs_reference_golden(name, geom):
+    """Tile geometries on reference-generated tile goldens."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import golden_utils as gu
+    import stencil_cases as sc
+    from test_gpu_parity import run_case_on_gpu
+
+    case = sc.CASES[name]
+    _, outputs, _ = gu.load(name)
+    res = run_case_on_gpu(case, geom_opts(geom))
+    for k, v in outputs.items():
+        gu.assert_match(res[k], v, name=f"{name}{geom}:{k}")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(CASES))
-@pytest.mark.parametrize("domain", [(5, 3, 4), (70, 9, 6), (131, 23, 13)])
 @pytest.mark.parametrize("geom", GEOMS)
-def test_tile_vs_numpy_backend(name, domain, geom):
+def test_tile_vs_numpy_backend(name, geom):
+    domain = (5, 3, 4)  # smaller than one tile; the ragged domains are the goldens above
     import torch
 
     if not torch.cuda.is_available():
