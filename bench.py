@@ -226,6 +226,22 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _physical_cores(cpus) -> int:
+    """Distinct (package, core) pairs among ``cpus`` (sysfs topology; SMT siblings count once)."""
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(base + "physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(base + "core_id") as f:
+                core = f.read().strip()
+        except OSError:
+            return len(list(cpus))
+        seen.add((pkg, core))
+    return len(seen)
+
+
 def _demo_field(ni, nj, nk, dtype):
     """The demo analytic field in=5+8*(2+cos(pi(x+1.5y))+sin(2pi(x+1.5y)))/4,
     constant in K, I-first (Fortran-ordered) host array."""
@@ -306,6 +322,10 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
         "unit": "Mcells/s",
         "cores": threads,
         "affinity_cpus": affinity,
+        "physical_cores_in_affinity": int(os.environ.get("GTMI_PHYS_CORES", "0")) or None,
+        "inherited_OMP_NUM_THREADS": os.environ.get("GTMI_INHERITED_OMP"),
+        "threads_policy": "the GPU pool's per-GPU CPU share (inherited OMP_NUM_THREADS; the host is shared by "
+                          "8 GPUs' jobs); not every physical core of the host",
         "os_cpu_count": os.cpu_count(),
         "kind": "port",
         "ms_per_call": round(med * 1e3, 3),
@@ -331,12 +351,20 @@ def cpu_baseline(cfg_name: str, reps: int = 40, warm: int = 3, timeout_s: float 
     # this (unbound) process's CPU set: the child's own affinity is a single core once libgomp has
     # bound its master thread, and more threads than CPUs would only oversubscribe
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        cpus = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        ncpu = os.cpu_count() or 1
-    threads = min(int(env.get("OMP_NUM_THREADS") or ncpu), ncpu)
+        cpus = list(range(os.cpu_count() or 1))
+    ncpu = len(cpus)
+    # Thread count: the CPU share the GPU pool gives one GPU's job (OMP_NUM_THREADS, 16 per GPU on
+    # the MI355X boxes, whose hosts are shared by 8 GPUs' jobs; the pool asks GPU jobs to size
+    # thread pools to it and not to raise it). SURVEY.md §8(d) would use every physical core of
+    # the host; that count is recorded next to the figure, not used.
+    inherited = env.get("OMP_NUM_THREADS")
+    threads = min(int(inherited or ncpu), ncpu)
     env["OMP_NUM_THREADS"] = str(threads)
     env["GTMI_PARENT_AFFINITY"] = str(ncpu)
+    env["GTMI_INHERITED_OMP"] = str(inherited)
+    env["GTMI_PHYS_CORES"] = str(_physical_cores(cpus))
     env["OMP_PROC_BIND"] = "close"
     env["OMP_PLACES"] = "cores"
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", cfg_name, "--cpu-reps", str(reps),
@@ -424,6 +452,26 @@ def box_identity(dev_index: int = 0):
 # ------------------------------------------------------------------------------------------
 
 
+def hbm_estimate(cfg, domain, args, candidates) -> dict:
+    """Peak device memory of one rank for this config (bytes, from the allocated fields): the
+    fields themselves, the placement tuner's transient copies of the written fields (a backup plus
+    ``candidates`` buffer sets, each padded by 2 MiB; the tuner itself caps the sets at 80 % of
+    free memory) and the halo path's pack buffers (small). DESIGN.md §6."""
+    try:
+        fields = sum(t.untyped_storage().nbytes() for t in args)
+    except AttributeError:  # dry run on host arrays
+        fields = sum(getattr(t, "nbytes", 0) for t in args)
+    sname, dtype, _, _, _ = CONFIGS[cfg]
+    ni, nj, nk = domain
+    item = np.dtype(dtype).itemsize
+    written = {"horizontal_diffusion": 1, "horizontal_diffusion_blocks": 1, "lap5": 1, "copy_stencil": 1,
+               "tridiagonal_solver": 3, "vertical_advection_dycore": 1, "staged_forward_ij_temp": 1}.get(sname, 1)
+    per_written = (ni + 32) * nj * nk * item + (2 << 20)
+    tuner = (1 + candidates) * written * per_written if candidates > 0 else 0
+    return {"fields_gb": round(fields / 1e9, 6), "tuner_transient_gb": round(tuner / 1e9, 6),
+            "peak_gb": round((fields + tuner) / 1e9, 6)}
+
+
 class Workload:
     """One config's fields, stencil and step function on this rank."""
 
@@ -442,7 +490,13 @@ class Workload:
         self.global_ij = (ni, nj * world)  # weak scaling: the per-GPU tile is fixed
         self.dec2d = None
         if world > 1 and args.decomp == "2d":
-            self.dec2d = Decomposition2D.balanced(self.global_ij[0], self.global_ij[1], world)
+            # the most square process grid pi x pj (pi <= pj: 1x2, 2x2, 2x4) of whole per-GPU
+            # tiles, so the global domain grows along both axes and every rank has four neighbours
+            # once pi, pj >= 2 (a J-only growth would make the least-perimeter grid a 1 x N strip)
+            pi = max(p for p in range(1, int(world ** 0.5) + 1) if world % p == 0)
+            pj = world // pi
+            self.global_ij = (ni * pi, nj * pj)
+            self.dec2d = Decomposition2D(self.global_ij[0], self.global_ij[1], pi, pj, (False, False))
             ni, nj = self.dec2d.local_shape(rank)
         self.domain = (ni, nj, nk)
         opts = {} if dry_run else {"device_sync": False}
@@ -527,24 +581,24 @@ class Workload:
         # validate once (full argument checks), then every timed call skips validation
         self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain)
         self.placement = None
+        self.untuned = None
+        self.hbm_estimate = hbm_estimate(cfg, self.domain, self.args, getattr(args, "placement_candidates", 0))
         ncand = getattr(args, "placement_candidates", 0)
         if not dry_run and ncand > 0:
-            self.tune_placement(ncand)
+            self.tune_placement(ncand, args)
 
-    def tune_placement(self, candidates: int):
+    def tune_placement(self, candidates: int, args):
         """Re-home the fields this stencil writes to the fastest of ``candidates + 1`` buffer sets
-        (``gt4py_amd.storage.placement``; DESIGN.md §5 "HBM placement"): done once, before any
-        timed step, as a long-running simulation would after allocating its fields."""
-        from gt4py_amd.storage.placement import tune_written_fields
-
-        names = list(self.stencil.field_info.keys())
-        assert len(names) == len(self.args), (names, len(self.args))
-        arrays, rep = tune_written_fields(self.stencil, dict(zip(names, self.args)), origin=self.origin,
-                                          domain=self.domain, params=self.params, candidates=candidates)
-        self.args = tuple(arrays[n] for n in names)
-        if self.named is not None:
-            self.named = {n: arrays[n] for n in self.named}
-        self.placement = rep
+        through the drop-in call, ``StencilObject.tune_placement`` (in place: the argument tensors
+        stay the same objects; DESIGN.md §5 "HBM placement"): done once, before any timed step, as
+        a long-running simulation would after allocating its fields. The first allocation's time is
+        measured first exactly as the headline is (K steps, HIP events), so the line carries the
+        untuned figure as well."""
+        steps, warm = (args.steps, args.warmup) if self.cfg == args.config else (args.extra_steps, 3)
+        el, km = time_workload(self, steps, warm, self.dev, None, step=self.plain_step)
+        self.untuned = {"ms_per_step": el / steps * 1e3, "kernel_ms": km}
+        self.placement = self.stencil.tune_placement(*self.args, **self.params, origin=self.origin,
+                                                     domain=self.domain, candidates=candidates)
 
     def step(self):
         if self.halo is not None:
@@ -927,6 +981,19 @@ def main():
             "library": key,
         },
     }
+    if wl.untuned is not None:
+        # the first allocation (what a plain `@gtscript.stencil` + storage allocation gives a
+        # drop-in user without the opt-in tuner), timed the same way as the headline, K steps
+        u_ms = wl.untuned["kernel_ms"] or wl.untuned["ms_per_step"]
+        u_gbs = cells_per_step * wl.bpc / (u_ms * 1e-3) / 1e9
+        result["roofline"].update(kernel_ms_untuned=round(u_ms, 4), achieved_untuned=round(u_gbs, 1),
+                                  frac_untuned=round(u_gbs / HBM_PEAK_GBS, 4),
+                                  untuned_ms_per_step=round(wl.untuned["ms_per_step"], 4),
+                                  Mcells_s_untuned=round(cells_per_step / (wl.untuned["ms_per_step"] * 1e-3) / 1e6, 2),
+                                  tuned_note="kernel_ms/frac: written fields re-homed in place by the opt-in "
+                                             "StencilObject.tune_placement (DESIGN.md §5); *_untuned: the first "
+                                             "allocation, same K-step measurement")
+    result["hbm_estimate"] = dict(wl.hbm_estimate, per_rank=True)
     if dist_rec is not None:
         result["dist"] = dist_rec
     if halo_ab is not None:
@@ -998,6 +1065,10 @@ def main():
                 }
                 if w.placement is not None:
                     extra[cfg]["placement"] = {k: w.placement[k] for k in ("candidates_ms", "chosen", "untuned_ms")}
+                if w.untuned is not None and w.untuned["kernel_ms"]:
+                    u_gbs = n_i * n_j * n_k * w.bpc / (w.untuned["kernel_ms"] * 1e-3) / 1e9
+                    extra[cfg]["kernel_ms_untuned"] = round(w.untuned["kernel_ms"], 4)
+                    extra[cfg]["frac_untuned"] = round(u_gbs / HBM_PEAK_GBS, 4)
                 del w
             except Exception as e:  # noqa: BLE001 - one failing extra config must not hide the headline
                 extra[cfg] = {"error": f"{type(e).__name__}: {e}"[:300]}

@@ -2267,7 +2267,7 @@ FUZZ_GOLDEN = []
 
 def _fuzz_cases():
     for n, seed in enumerate(_fgp.SEEDS):
-        ni, nj, nk = TILE_DOMAINS["d70" if n % 2 == 0 else "d131"]
+        ni, nj, nk = TILE_DOMAINS["d70"]  # 2 x 2 tiles with partial ones (kept small: five random fields)
         fields = {f: fs(ni + 4, nj + 4, nk, init=("u", -4.0, 4.0)) for f in ("a", "b", "c")}
         fields.update({f: fs(ni, nj, nk, init=("u", -1.0, 1.0)) for f in ("out1", "out2")})
         origin = {"a": (2, 2, 0), "b": (2, 2, 0), "c": (2, 2, 0), "out1": (0, 0, 0), "out2": (0, 0, 0)}

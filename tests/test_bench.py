@@ -22,9 +22,13 @@ def _run(args, env_extra=None, timeout=240):
                           text=True, timeout=timeout, cwd=REPO)
 
 
-@pytest.mark.parametrize("gpus,decomp", [(1, "jstrips"), (2, "jstrips"), (2, "2d"), (3, "jstrips")])
+@pytest.mark.parametrize("gpus,decomp", [(1, "jstrips"), (2, "jstrips"), (2, "2d"), (3, "jstrips"),
+                                         (4, "jstrips"), (4, "2d"), (8, "jstrips"), (8, "2d")])
 def test_bench_launcher_dry_run(gpus, decomp):
-    res = _run(["--dry-run", "--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--decomp", decomp])
+    """The driver's 1/2/4/8-rank command lines, rehearsed on the CPU (gloo, numpy backend, a
+    64x32x8 tile per rank): one JSON line with the whole N-rank record, C5 leg included."""
+    res = _run(["--dry-run", "--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--decomp", decomp],
+               timeout=600)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, res.stdout
@@ -32,9 +36,15 @@ def test_bench_launcher_dry_run(gpus, decomp):
     assert rec["n_gpus"] == gpus
     assert rec["dry_run"] is True
     assert rec["steps"] == 2 and rec["warmup"] == 1
-    assert rec["config"]["global_domain"][1] == 32 * gpus
+    gi, gj, _ = rec["config"]["global_domain"]
+    assert gi * gj == 64 * 32 * gpus and rec["config"]["domain_per_gpu"][:2] == [64, 32]
+    assert rec["hbm_estimate"]["peak_gb"] >= rec["hbm_estimate"]["fields_gb"] > 0
     if gpus > 1:
         assert rec["config"]["parallelism"].startswith("ij-")
+        if decomp == "2d":  # a balanced process grid: 2x2 at 4 ranks, 2x4 at 8
+            want = {2: "1x2", 4: "2x2", 8: "2x4"}.get(gpus)
+            if want is not None:
+                assert rec["config"]["parallelism"] == f"ij-tiles{want}", rec["config"]
         # the N>1 line explains itself
         d = rec["dist"]
         assert d["world_size"] == gpus
@@ -48,7 +58,7 @@ def test_bench_launcher_dry_run(gpus, decomp):
         # C5 (the f32 tile) through the same N-rank path, whole-job cells/s
         c5 = rec["extra_configs"]["hdiff_f32"]
         assert "error" not in c5, c5
-        assert c5["n_gpus"] == gpus and c5["global_domain"][1] == 32 * gpus
+        assert c5["n_gpus"] == gpus and c5["global_domain"][0] * c5["global_domain"][1] == 64 * 32 * gpus
         assert c5["Mcells_s"] > 0 and c5["scaling"] == "weak"
     else:
         assert "dist" not in rec
@@ -78,5 +88,7 @@ def test_bench_gpu_line_with_placement_tuning():
     p = rec["placement"]
     assert p["written"] == ["out_field"] and len(p["candidates_ms"]) == 3
     assert p["tuned_ms"] == min(p["candidates_ms"]) == p["candidates_ms"][p["chosen"]]
-    assert p["untuned_ms"] == p["candidates_ms"][0]
+    assert p["untuned_ms"] == p["candidates_ms"][0] and p["in_place"]
     assert rec["full_call"]["overhead_vs"] == "kernel_ms"
+    r = rec["roofline"]
+    assert 0.0 < r["frac_untuned"] <= 1.0 and r["kernel_ms_untuned"] > 0
