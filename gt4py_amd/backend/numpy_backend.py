@@ -189,12 +189,39 @@ class NumpyExecutor:
                 for x in s.body:
                     self._stmt(x, reg, m)
         elif isinstance(s, ir.HorizontalRegion):
-            rm = self._region_mask(s.masks, reg)
-            m = rm if mask is None else (mask & rm)
-            for x in s.body:
-                self._stmt(x, reg, m)
+            # each mask in turn over its own sub-box of ``reg`` (the reference numpy backend's
+            # relative masks, gtc/passes/horizontal_masks.py:98-115): the body only touches points
+            # inside the region, so fields need no halo beyond the region's clipped extent
+            for hm in s.masks:
+                sub = self._region_box(hm, reg)
+                if sub is None:
+                    continue
+                m = None
+                if mask is not None:
+                    i0, _, j0, _, _, _ = reg
+                    m = np.broadcast_to(mask, _shape(reg))[sub[0] - i0:sub[1] - i0, sub[2] - j0:sub[3] - j0]
+                for x in s.body:
+                    self._stmt(x, sub, m)
         else:
             raise TypeError(type(s))
+
+    def _region_box(self, hm, reg):
+        """``reg`` restricted to the rectangle of horizontal mask ``hm`` (None if empty)."""
+        ni, nj, _ = self.domain
+        i0, i1, j0, j1, k0, k1 = reg
+
+        def lim(itv, n, a, b):
+            if itv.start is not None:
+                a = max(a, itv.start.offset if itv.start.level == ir.LevelMarker.START else n + itv.start.offset)
+            if itv.end is not None:
+                b = min(b, itv.end.offset if itv.end.level == ir.LevelMarker.START else n + itv.end.offset)
+            return a, b
+
+        a0, a1 = lim(hm.i, ni, i0, i1)
+        b0, b1 = lim(hm.j, nj, j0, j1)
+        if a1 <= a0 or b1 <= b0:
+            return None
+        return (a0, a1, b0, b1, k0, k1)
 
     def _region_mask(self, masks, reg):
         ni, nj, _ = self.domain

@@ -20,23 +20,68 @@ struct LaunchBoxes {
 
 static thread_local char g_err[512];
 
+// A box is ej*ek ROWS of ei elements contiguous along I (the field's I stride) and along the
+// buffer. Narrow boxes (the I faces of a 2-D exchange: ei = halo width, one or two 8-B cells per
+// row) take one row per lane, so a wave touches 64 rows with no index math per element; wide
+// boxes (J faces: whole rows) take 64-element chunks of a row per wave, coalesced along I. Row and
+// chunk indices are computed once per lane (narrow, 32-bit when the box allows) or once per wave
+// in scalar registers (wide), not per element: the round-2 kernel's three 64-bit divisions per
+// element dominated the narrow I faces.
+#define GTMI_HALO_NARROW 16
+
+template <typename T>
+__device__ __forceinline__ void copy_row(const gtmi_box& bx, int64_t row, int64_t i0, int64_t n, int direction,
+                                         int64_t step) {
+    const int64_t ej = bx.extent[1], ei = bx.extent[0];
+    const int64_t j = row % ej, k = row / ej;
+    T* __restrict__ f = (T*)bx.field +
+                        ((bx.start[1] + j) * bx.strides[1] + (bx.start[2] + k) * bx.strides[2] + bx.start[0] * bx.strides[0]);
+    T* __restrict__ buf = (T*)bx.buffer + row * ei;
+    const int64_t si = bx.strides[0];
+    if (direction == 0) {
+        for (int64_t i = i0; i < n; i += step) buf[i] = f[i * si];
+    } else {
+        for (int64_t i = i0; i < n; i += step) f[i * si] = buf[i];
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ void copy_box(const gtmi_box& bx, int direction) {
     const int64_t ei = bx.extent[0], ej = bx.extent[1], ek = bx.extent[2];
-    const int64_t n = ei * ej * ek;
-    T* __restrict__ f = (T*)bx.field;
-    T* __restrict__ buf = (T*)bx.buffer;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = e % ei;
-        const int64_t r = e / ei;
-        const int64_t j = r % ej;
-        const int64_t k = r / ej;
-        const int64_t off = (bx.start[0] + i) * bx.strides[0] + (bx.start[1] + j) * bx.strides[1] +
-                            (bx.start[2] + k) * bx.strides[2];
-        if (direction == 0)
-            buf[e] = f[off];
-        else
-            f[off] = buf[e];
+    const int64_t rows = ej * ek;
+    if (ei <= 0 || rows <= 0) return;
+    if (ei <= GTMI_HALO_NARROW) {
+        const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+        int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (rows <= 0xffffffffLL && ej <= 0xffffffffLL) {  // 32-bit row -> (j, k)
+            const uint32_t uej = (uint32_t)ej;
+            for (; r < rows; r += nthreads) {
+                const uint32_t ur = (uint32_t)r, j = ur % uej, k = ur / uej;
+                T* __restrict__ f = (T*)bx.field + ((bx.start[1] + j) * bx.strides[1] + (bx.start[2] + k) * bx.strides[2] +
+                                                    bx.start[0] * bx.strides[0]);
+                T* __restrict__ buf = (T*)bx.buffer + r * ei;
+                if (direction == 0) {
+                    for (int64_t i = 0; i < ei; ++i) buf[i] = f[i * bx.strides[0]];
+                } else {
+                    for (int64_t i = 0; i < ei; ++i) f[i * bx.strides[0]] = buf[i];
+                }
+            }
+        } else {
+            for (; r < rows; r += nthreads) copy_row<T>(bx, r, 0, ei, direction, 1);
+        }
+        return;
+    }
+    // wide: one wave per (row, 64-element chunk); wave-uniform indices in scalar registers
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t cpr = (ei + 63) / 64;
+    const int64_t units = rows * cpr;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int64_t u = w0; u < units; u += nwaves) {
+        const int64_t row = u / cpr, c = u - row * cpr;
+        const int64_t i0 = c * 64 + lane;
+        const int64_t n = (c + 1) * 64 < ei ? (c + 1) * 64 : ei;
+        copy_row<T>(bx, row, i0, n, direction, 64);
     }
 }
 
@@ -88,7 +133,15 @@ static int halo_copy_impl(const gtmi_box* boxes, int32_t n_boxes, int32_t direct
             if (n > maxn) maxn = n;
         }
         if (maxn == 0) continue;
-        int64_t blocks = (maxn + 255) / 256;
+        // work units of the largest box: rows (narrow boxes, one per lane) or 64-element row
+        // chunks (wide boxes, one per wave)
+        int64_t units = 0;
+        for (int b = 0; b < nb; ++b) {
+            const int64_t ei = lb.b[b].extent[0], rows = lb.b[b].extent[1] * lb.b[b].extent[2];
+            const int64_t lanes = ei <= GTMI_HALO_NARROW ? rows : rows * ((ei + 63) / 64) * 64;
+            if (lanes > units) units = lanes;
+        }
+        int64_t blocks = (units + 255) / 256;
         if (blocks > 2048) blocks = 2048;  // grid-stride beyond: ~8 waves per CU per box
         hipLaunchKernelGGL(gtmi_halo_kernel, dim3((unsigned)blocks, (unsigned)nb), dim3(256), 0, stream, lb, nb,
                            (int)direction);

@@ -20,6 +20,7 @@ Literal precision follows ``literal_int_precision``/``literal_float_precision``
 from __future__ import annotations
 
 import ast
+import copy
 import dataclasses
 import builtins
 import inspect
@@ -458,7 +459,10 @@ class StencilParser:
                     raise GTScriptSyntaxError(
                         f"{where} The following variables are written before being referenced with an offset in "
                         f"a horizontal region: {', '.join(bad)}")
-                return [ir.HorizontalRegion(masks, body)]
+                # one region statement per mask, in order, as the reference emits one HorizontalIf
+                # per region with the same body (gtscript_frontend.py:1957-1962): a point inside
+                # two overlapping masks runs the body twice
+                return [ir.HorizontalRegion([m], body if n == 0 else copy.deepcopy(body)) for n, m in enumerate(masks)]
             raise GTScriptSyntaxError(f"Invalid 'with' statement inside a computation (line {s.lineno})")
         if isinstance(s, ast.Return):
             raise GTScriptSyntaxError("'return' is only allowed in gtscript functions")

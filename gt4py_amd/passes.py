@@ -335,10 +335,31 @@ def iter_accesses(stmts):
 
 
 def compute_access_kinds(stencil: ir.Stencil) -> Dict[str, AccessKind]:
+    """First access decides READ / WRITE, a later write makes READ_WRITE; the body of a horizontal
+    region that cannot overlap its statement's (signed) extent is not visited
+    (``oir_access_kinds.py:43-48``)."""
     access: Dict[str, AccessKind] = {}
-    for vl in stencil.vertical_loops:
-        for sec in vl.sections:
-            for acc, is_write in iter_accesses(sec.body):
+    blocks: dict = {}
+    compute_signed_extents(stencil, blocks)
+
+    def visible(stmts, he):
+        for s in stmts:
+            if isinstance(s, ir.HorizontalRegion):
+                if any(mask_overlap(m, he) is not None for m in s.masks):
+                    yield from visible(s.body, he)
+            elif isinstance(s, (ir.If, ir.While)):
+                yield type(s)(s.cond, [], []) if isinstance(s, ir.If) else type(s)(s.cond, [])
+                yield from visible(s.body, he)
+                if isinstance(s, ir.If):
+                    yield from visible(s.orelse, he)
+            else:
+                yield s
+
+    for li, vl in enumerate(stencil.vertical_loops):
+        for si, sec in enumerate(vl.sections):
+            stmts = [x for ti, s in enumerate(sec.body)
+                     for x in visible([s], blocks.get((li, si, ti), ((0, 0), (0, 0))))]
+            for acc, is_write in iter_accesses(stmts):
                 kind = AccessKind.WRITE if is_write else AccessKind.READ
                 if kind == AccessKind.WRITE and access.get(acc.name) == AccessKind.READ:
                     access[acc.name] = AccessKind.READ_WRITE
@@ -366,6 +387,64 @@ def extent_shift(e: Extent, offset) -> Extent:
     return ((max(0, e[0][0] - di), max(0, e[0][1] + di)), (max(0, e[1][0] - dj), max(0, e[1][1] + dj)))
 
 
+def _overlap_along_axis(ext, itv) -> Optional[Tuple[int, int]]:
+    """Distances of a region interval to the edges of a (signed) extent, or None when the region
+    cannot overlap it (reference ``gtc/passes/horizontal_masks.py:15-47``)."""
+    if itv.start is None:
+        start_diff = 1000
+    elif itv.start.level == ir.LevelMarker.START:
+        start_diff = ext[0] - itv.start.offset
+    else:
+        start_diff = None
+    if itv.end is None:
+        end_diff = -1000
+    elif itv.end.level == ir.LevelMarker.END:
+        end_diff = ext[1] - itv.end.offset
+    else:
+        end_diff = None
+    if start_diff is not None and start_diff > 0 and end_diff is None and itv.end is not None:
+        if itv.end.offset <= ext[0]:
+            return None
+    elif end_diff is not None and end_diff < 0 and start_diff is None and itv.start is not None:
+        if itv.start.offset > ext[1]:
+            return None
+    start_diff = min(start_diff, 0) if start_diff is not None else -10000
+    end_diff = max(end_diff, 0) if end_diff is not None else 10000
+    return start_diff, end_diff
+
+
+def mask_overlap(mask, he_signed) -> Optional[Extent]:
+    """``mask_overlap_with_extent`` (horizontal_masks.py:50-58) on a signed extent."""
+    di = _overlap_along_axis(he_signed[0], mask.i)
+    dj = _overlap_along_axis(he_signed[1], mask.j)
+    return None if di is None or dj is None else (di, dj)
+
+
+def region_access_extent(masks, he_signed, di: int, dj: int) -> Optional[Extent]:
+    """Signed extent of a read at (di, dj) inside horizontal regions ``masks`` of a statement
+    with signed horizontal extent ``he_signed``: ``((he - dist_from_edge) + offset) | zeros``
+    per mask (``GenericAccess.to_extent``, oir_optimizations/utils.py:50-75), unioned; None when
+    no mask overlaps (the access then reads nothing)."""
+    out = None
+    for m in masks:
+        d = mask_overlap(m, he_signed)
+        if d is None:
+            continue
+        e = ((min(he_signed[0][0] - d[0][0] + di, 0), max(he_signed[0][1] - d[0][1] + di, 0)),
+             (min(he_signed[1][0] - d[1][0] + dj, 0), max(he_signed[1][1] - d[1][1] + dj, 0)))
+        out = e if out is None else ((min(out[0][0], e[0][0]), max(out[0][1], e[0][1])),
+                                     (min(out[1][0], e[1][0]), max(out[1][1], e[1][1])))
+    return out
+
+
+def _to_signed(e: Extent) -> Extent:
+    return ((-e[0][0], e[0][1]), (-e[1][0], e[1][1]))
+
+
+def _to_centered(e: Extent) -> Extent:
+    return ((max(0, -e[0][0]), max(0, e[0][1])), (max(0, -e[1][0]), max(0, e[1][1])))
+
+
 @dataclasses.dataclass
 class ExtentInfo:
     fields: Dict[str, Extent]
@@ -387,20 +466,27 @@ def compute_extents(stencil: ir.Stencil) -> ExtentInfo:
                     if is_write:
                         he = extent_union(he, fields.setdefault(acc.name, ZERO_EXTENT))
                 blocks[(li, si, ti)] = he
-                for acc, is_write in accesses:
+                for acc, is_write, masks in _accesses_with_region([stmt]):
                     if isinstance(acc, ir.FieldAccess):
-                        ext = extent_shift(he, acc.offset)
+                        if masks is None:
+                            ext = extent_shift(he, acc.offset)
+                        else:  # inside a horizontal region: clipped by its mask (reference semantics)
+                            se = region_access_extent(masks, _to_signed(he), acc.offset[0], acc.offset[1])
+                            if se is None:
+                                continue
+                            ext = _to_centered(se)
                         fields[acc.name] = extent_union(fields.get(acc.name, ZERO_EXTENT), ext)
     for p in stencil.params:
         fields.setdefault(p.name, ZERO_EXTENT)
     return ExtentInfo(fields, blocks)
 
 
-def _accesses_with_region(stmts, in_region=False):
-    """(access, is_write, inside a horizontal region) in :func:`iter_accesses` order."""
+def _accesses_with_region(stmts, in_region=None):
+    """(access, is_write, masks of the enclosing horizontal region or None) in
+    :func:`iter_accesses` order."""
     for s in stmts:
         if isinstance(s, ir.HorizontalRegion):
-            yield from _accesses_with_region(s.body, True)
+            yield from _accesses_with_region(s.body, s.masks)
         elif isinstance(s, (ir.If, ir.While)):
             for acc, w in iter_accesses([type(s)(s.cond, [], []) if isinstance(s, ir.If) else type(s)(s.cond, [])]):
                 yield acc, w, in_region
@@ -412,34 +498,44 @@ def _accesses_with_region(stmts, in_region=False):
                 yield acc, w, in_region
 
 
-def compute_signed_extents(stencil: ir.Stencil) -> Dict[str, Extent]:
+def compute_signed_extents(stencil: ir.Stencil, blocks_out: Optional[dict] = None) -> Dict[str, Extent]:
     """Per-field extents as signed offset ranges ``((i_min, i_max), (j_min, j_max))``, the
     non-centered extents the reference reports in ``FieldInfo.boundary``
     (``oir_optimizations/utils.py:250-315``: a read at ``he + offset`` is NOT widened to include
     offset 0, so a field read only at ``[1, 0, 0]`` gets the boundary ``(-1, 1)`` in I and may be
-    called with origin -1; accesses inside horizontal regions are widened to 0). Code generation
-    keeps using the centered halo sizes of :func:`compute_extents`."""
+    called with origin -1; accesses inside horizontal regions are clipped by the region's mask and
+    widened to 0, ``GenericAccess.to_extent``). Code generation keeps using the centered halo
+    sizes of :func:`compute_extents`. ``blocks_out``: filled with the signed statement extents
+    ((loop, section, statement) -> extent, ``compute_horizontal_block_extents``)."""
     zero = ((0, 0), (0, 0))
 
     def union(a, b):
         return ((min(a[0][0], b[0][0]), max(a[0][1], b[0][1])), (min(a[1][0], b[1][0]), max(a[1][1], b[1][1])))
 
     fields: Dict[str, Extent] = {}
-    for vl in reversed(stencil.vertical_loops):
-        for sec in reversed(vl.sections):
-            for stmt in reversed(sec.body):
+    for li in reversed(range(len(stencil.vertical_loops))):
+        vl = stencil.vertical_loops[li]
+        for si in reversed(range(len(vl.sections))):
+            sec = vl.sections[si]
+            for ti in reversed(range(len(sec.body))):
+                stmt = sec.body[ti]
                 accesses = list(_accesses_with_region([stmt]))
                 he = zero
                 for acc, is_write, _ in accesses:
                     if is_write:
                         he = union(he, fields.setdefault(acc.name, zero))
-                for acc, _, in_region in accesses:
+                if blocks_out is not None:
+                    blocks_out[(li, si, ti)] = he
+                for acc, _, masks in accesses:
                     if not isinstance(acc, ir.FieldAccess):
                         continue
                     di, dj = acc.offset[0], acc.offset[1]
-                    ext = ((he[0][0] + di, he[0][1] + di), (he[1][0] + dj, he[1][1] + dj))
-                    if in_region:
-                        ext = union(ext, zero)
+                    if masks is None:
+                        ext = ((he[0][0] + di, he[0][1] + di), (he[1][0] + dj, he[1][1] + dj))
+                    else:
+                        ext = region_access_extent(masks, he, di, dj)
+                        if ext is None:
+                            continue
                     fields[acc.name] = union(fields[acc.name], ext) if acc.name in fields else ext
     for p in stencil.params:
         fields.setdefault(p.name, zero)

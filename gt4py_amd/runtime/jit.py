@@ -89,6 +89,10 @@ def compile_source(source: str, extra_flags: Optional[List[str]] = None, verbose
     key = build_key(source, extra_flags)
     d = os.path.join(cache_root(), key)
     so = os.path.join(d, "stencil.so")
+    log = os.environ.get("GTMI_CACHE_LOG")
+    if log:  # scripts/prune_cache.py: which entries a build still uses
+        with open(log, "a") as f:
+            f.write(key + "\n")
     if os.path.exists(so):
         return so
     if os.environ.get("GTMI_NO_COMPILE"):

@@ -2054,6 +2054,30 @@ case(
 )(horizontal_region_with_conditional)
 
 
+def region_offset_reads(a: F64, b: F64, out: F64):
+    """Offset reads inside horizontal regions near the domain edges: the reference clips each
+    read's extent by its region's mask (oir_optimizations/utils.py:50-75), so ``b`` needs no
+    west halo although it is read at ``[-1, 0, 0]``; overlapping masks of one ``with`` run the
+    body once per mask (gtscript_frontend.py:1957-1962): the corner (0, 0) gets +2."""
+    with computation(PARALLEL), interval(...):
+        out = a
+        with horizontal(region[I[-1] - 2 : I[-1], :]):
+            out = b[-1, 0, 0] + a[0, 1, 0]
+        with horizontal(region[I[0] + 1 : I[0] + 3, J[-1] - 1 : J[-1]]):
+            out = out - b[1, 0, 0] * a[-1, 0, 0]
+        with horizontal(region[I[0], :], region[:, J[0]]):
+            out = out + 1.0
+
+
+case(
+    "region_offset_reads",
+    fields={"a": fs(13, 11, 4), "b": fs(13, 11, 4), "out": fs(9, 7, 4, init="zeros")},
+    origin={"a": (2, 2, 0), "b": (2, 2, 0), "out": (0, 0, 0)},
+    domain=(9, 7, 4),
+    features=("regions",),
+)(region_offset_reads)
+
+
 # --------------------------------------------------------------------------------------
 # Column-kernel schedule edge cases (gt:mi355x K2: load ring, LDS tail cache, section gaps)
 # --------------------------------------------------------------------------------------
