@@ -57,7 +57,10 @@ def _digest() -> str:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(torch.__version__.encode())
-    h.update(" ".join(_command(target_path())).encode())
+    # the command with the repository's own paths made relative: the tree is built here and run
+    # from another directory on the GPU box
+    repo = os.path.dirname(_PKG)
+    h.update(" ".join(c.replace(repo, "<repo>") for c in _command(target_path())).encode())
     return h.hexdigest()[:24]
 
 

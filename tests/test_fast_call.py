@@ -331,3 +331,28 @@ def test_native_prepared_rejects_other_arguments():
     with pytest.raises(ValueError):
         m.Prepared(0, 0, (4, 3, 2), ctypes.addressof(fields), 2, ctypes.addressof(scal), 1, [(5, 0, 0)], 1,
                    [x, y], 0, False, "t")
+
+
+def test_native_module_survives_a_moved_tree(tmp_path):
+    """The built extension's stamp must not depend on where the tree lives: the GPU box runs the
+    tree from another directory (round 4: an absolute path in the digest made every box see a
+    'stale' module and fall back to the ctypes launch)."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+
+    from gt4py_amd.runtime import fastcall
+
+    if not fastcall.up_to_date():
+        pytest.skip("gt4py_amd._gtmi_fastcall not built")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(fastcall.__file__)))
+    repo = os.path.dirname(repo)
+    shutil.copytree(os.path.join(repo, "gt4py_amd"), tmp_path / "gt4py_amd",
+                    ignore=shutil.ignore_patterns("__pycache__"))
+    shutil.copytree(os.path.join(repo, "include"), tmp_path / "include")
+    code = ("import warnings; warnings.simplefilter('error'); from gt4py_amd.runtime import fastcall; "
+            "assert fastcall.up_to_date(); assert fastcall.module() is not None")
+    res = subprocess.run([sys.executable, "-c", code], cwd=tmp_path, capture_output=True, text=True,
+                         env={k: v for k, v in os.environ.items() if k != "PYTHONPATH"})
+    assert res.returncode == 0, res.stderr[-2000:]
