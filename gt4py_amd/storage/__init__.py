@@ -176,7 +176,9 @@ def allocate_gpu(shape, layout_map, dtype, alignment_bytes, aligned_index):
     strides, shift, total, align_el = _allocation_plan(
         shape, layout_map, dtype.itemsize, alignment_bytes, aligned_index
     )
-    residue = hbm_stagger_residue(total * dtype.itemsize)
+    # the stagger keeps the alignment only when the alignment divides its 2-quantum period (every
+    # backend's 256 B does; an arbitrary alignment such as 152 B gets plain alignment)
+    residue = hbm_stagger_residue(total * dtype.itemsize) if (2 * HBM_STAGGER_QUANTUM) % alignment_bytes == 0 else None
     extra = align_el if residue is None else (2 * HBM_STAGGER_QUANTUM) // dtype.itemsize + align_el
     buf = torch.empty(int(total + extra), dtype=torch_dtype(dtype), device=dev.current_device())
     if residue is None:
