@@ -623,10 +623,12 @@ class ColumnGen:
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
             self._kaddr = kaddr
 
-            def shift_and_fronts(slot: Optional[int], mode: str, reg_u: Optional[int] = None) -> List[str]:
+            def shift_and_fronts(slot: Optional[int], mode: str, reg_u: Optional[int] = None,
+                                 pf: Optional[Dict] = None) -> List[str]:
                 """Shift every window one level and load each front: from ring ``slot``, from the
                 LDS tail cache (``mode`` "lds"), from the register band (``reg_u``: the level's band
-                index) or from memory here (``slot`` None)."""
+                index), from a band prefetch register (``pf``: key -> variable) or from memory here
+                (``slot`` None)."""
                 body = []
                 for key, rng in win.items():
                     name, di, dj = key
@@ -640,7 +642,9 @@ class ColumnGen:
                     if front_load[key]:
                         fd = front[key]
                         fv = wvar(name, di, dj, fd)
-                        if reg_u is not None:
+                        if pf is not None and key in pf:
+                            body.append(f"{fv} = {pf[key]};")
+                        elif reg_u is not None:
                             body += load_into(fv, name, di, dj, f"k + ({fd})", maybe_cached=False, reg=reg_u + fd)
                         elif mode == "lds" and key in tail_keys:
                             body.append(f"{fv} = {tail.var(name)}[(k + ({fd}) - tc0) * 256 + tid];")
@@ -820,16 +824,52 @@ class ColumnGen:
             out.append("    }")
             us = [u for u in range(R) if band_map[u] == si] if R else []
             if us:
-                # this section's register-band levels: unrolled, static register names
+                # this section's register-band levels: unrolled, static register names. The band
+                # is straight-line code, so its memory fronts are software-pipelined explicitly:
+                # band level n's fronts are loaded ``kreg_pf`` band levels earlier into registers
+                # of their own (a level waiting for its own loads stalls a one-wave-per-SIMD kernel)
+                order_us = sorted(us, reverse=not fwd)
+                kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
+                Pb = int(self.opts.get("kreg_pf", P))
+                mem_keys = {}
+                for u in order_us:
+                    mk = []
+                    for key in win:
+                        if not front_load[key] or not self._mem(key[0]):
+                            continue
+                        fd = front[key]
+                        if key[0] in tail_read and key[1:] == (0, 0) and 0 <= u + fd < R:
+                            continue  # served by the register band
+                        mk.append(key)
+                    mem_keys[u] = mk
                 bc = [f"    if (regband) {{  // section {si}: register band levels"]
-                for n_, u in enumerate(sorted(us, reverse=not fwd)):
-                    kexpr = f"nk - {R} + {u}" if tail.a_fwd else f"{u}"
+                pfv = {}
+                if Pb > 0:
+                    for u in order_us:
+                        for key in mem_keys[u]:
+                            t_ = decl_dtype[key[0]].ctype
+                            pfv[(u, key)] = f"bp{u}_{wvar(*key, front[key])}"
+                            bc.append(f"        {t_} {pfv[(u, key)]};")
+
+                def prefetch(u_):
+                    return [f"{pfv[(u_, key)]} = {mem_index(key[0], key[1], key[2], f'({kexpr_of(u_)}) + ({front[key]})')};"
+                            for key in mem_keys[u_]]
+
+                if Pb > 0:
+                    bc.append("        // band prefetch prologue")
+                    for u in order_us[:Pb]:
+                        bc += ["        " + x for x in prefetch(u)]
+                for n_, u in enumerate(order_us):
+                    kexpr = kexpr_of(u)
                     reg_now[0], band_now[0] = u, "reg"
+                    pf = {key: pfv[(u, key)] for key in mem_keys[u]} if Pb > 0 else None
                     if n_ == 0:
                         body = (["if (k != k_next) {"] + ["    " + x for x in reload(u)] + ["} else {"]
-                                + ["    " + x for x in shift_and_fronts(None, "mem", u)] + ["}"])
+                                + ["    " + x for x in shift_and_fronts(None, "mem", u, pf)] + ["}"])
                     else:
-                        body = shift_and_fronts(None, "mem", u)
+                        body = shift_and_fronts(None, "mem", u, pf)
+                    if Pb > 0 and n_ + Pb < len(order_us):
+                        body += prefetch(order_us[n_ + Pb])
                     body += statements()
                     reg_now[0], band_now[0] = None, None
                     bc.append(f"        {{  const int k = {kexpr};")

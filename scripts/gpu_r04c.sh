@@ -9,9 +9,9 @@ mkdir -p gpurun_out
 if [ "${TESTS:-1}" = 1 ]; then
   bash scripts/gpu_tests.sh || exit $?
 fi
-timeout -k 10 300 python -u scripts/sweep.py --config vadv --variants "kreg=0;kreg=48;kreg=64;kreg=80;kreg=96;kreg=112" \
+timeout -k 10 300 python -u scripts/sweep.py --config vadv --variants "kreg=0;kreg=32;kreg=64;kreg=96;kreg=112;kreg=64,kreg_pf=0;kreg=96,kreg_pf=4" \
   --rounds 6 > gpurun_out/r04c_sweep_vadv_kreg.log 2>&1 || { tail -30 gpurun_out/r04c_sweep_vadv_kreg.log; exit 1; }
 cat gpurun_out/r04c_sweep_vadv_kreg.log
-timeout -k 10 300 python -u scripts/sweep.py --config tridiag --variants "kreg=0;kreg=48;kreg=64;kreg=96;kreg=112" \
+timeout -k 10 300 python -u scripts/sweep.py --config tridiag --variants "kreg=0;kreg=32;kreg=64;kreg=96;kreg=112;kreg=64,kreg_pf=0;kreg=96,kreg_pf=4" \
   --rounds 6 > gpurun_out/r04c_sweep_tridiag_kreg.log 2>&1 || { tail -30 gpurun_out/r04c_sweep_tridiag_kreg.log; exit 1; }
 cat gpurun_out/r04c_sweep_tridiag_kreg.log

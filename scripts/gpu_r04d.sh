@@ -15,3 +15,7 @@ export RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533
 for d in jstrips 2d jstrips 2d; do
   timeout -k 10 300 python3 bench.py --no-extra --no-cpu-baseline --steps 50 --halo-selfcomm --decomp $d --placement-candidates 0 2>> $O/halo.err | tee -a $O/halo.log || exit 1
 done
+unset RANK LOCAL_RANK WORLD_SIZE MASTER_ADDR MASTER_PORT
+# the N>1 path with in-place placement tuning in every rank (2 ranks on one GPU over gloo)
+bash scripts/dist_rehearsal.sh > $O/dist_rehearsal.log 2>&1 || { tail -30 $O/dist_rehearsal.log; exit 1; }
+cp gpurun_out/dist_*.json $O/ && cat $O/dist_rehearsal.log | tail -4

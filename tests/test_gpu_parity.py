@@ -102,7 +102,8 @@ def test_golden_case(name):
 COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tail_bwd_fwd", "tail_bwd_fwd_short",
                     "tail_fwd_bwd_offsets", "tridiag", "tridiag_k161", "tridiag_k2", "tridiag_k70",
                     "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80"]
-COLUMN_OPTS = [{"kreg": 32}, {"kreg": 16, "seg_tail": 1}, {"seg_tail": 1}, {"ktail_lds": 0}, {"kring": 3}]
+COLUMN_OPTS = [{"kreg": 32}, {"kreg": 16, "seg_tail": 1}, {"seg_tail": 1}, {"ktail_lds": 0}, {"kring": 3},
+               {"kreg": 96}, {"kreg": 64, "kreg_pf": 0}, {"kreg": 48, "kreg_pf": 3}]
 
 
 @pytest.mark.parametrize("opts", COLUMN_OPTS, ids=lambda o: "_".join(f"{k}{v}" for k, v in o.items()))
