@@ -36,7 +36,9 @@ from gt4py_amd.codegen.common import (  # noqa: F401
 
 LDS_BYTES = 160 * 1024  # per CU (MI355X_MICROARCH.md); one 256-thread block may take all of it
 DEFAULT_RING = 8
-DEFAULT_KREG = 0  # register band levels (option ``kreg``)
+# register band levels (option ``kreg``; -1 = auto, see ColumnGen._plan_register_band)
+DEFAULT_KREG = -1
+AUTO_KREG = 96
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -274,6 +276,16 @@ class ColumnGen:
         below it the kernel runs without the register band)."""
         self.kreg = 0
         R = int(self.opts.get("kreg", DEFAULT_KREG))
+        if R < 0:
+            # auto: a band of AUTO_KREG levels when every cached field is a scratch temporary that
+            # the band keeps out of memory altogether (no write, no re-read: 32 B per level and
+            # column for two f64 fields) and the cached bytes per level fit two f64: vadv
+            # 1024^2x160 2.42 -> 1.885 ms (kreg 96, band fronts prefetched 8 levels ahead; 32: 2.11,
+            # 64: 2.00, 112: 1.94 ms). When the cached fields are API outputs (tridiag's sup/rhs,
+            # written anyway) the band saves only the re-read and costs more than it saves
+            # (kreg 32: -1.3 %, 64: +5 %, 96: +35 %), so no band (profiles/r04/r04c_sweep_*_kreg.log)
+            per_level = sum(self.st.decl(n).dtype.itemsize for n in t.fields)
+            R = AUTO_KREG if (t.fields and all(n in t.no_store for n in t.fields) and per_level <= 16) else 0
         if R <= 0:
             return
         B = self.info[t.b]

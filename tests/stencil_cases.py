@@ -2107,6 +2107,21 @@ case(
 )(vertical_advection_dycore)
 
 
+case(
+    "vertical_advection_dycore_k160",  # long enough for the register band of the column kernel (auto: 96 levels)
+    fields={
+        "utens_stage": fs(9, 6, 160),
+        "u_stage": fs(9, 6, 160),
+        "wcon": fs(10, 6, 161, init=("u", -1.0, 1.0)),
+        "u_pos": fs(9, 6, 160),
+        "utens": fs(9, 6, 160),
+    },
+    params={"dtr_stage": 3.0 / 20.0},
+    externals={"BET_M": 0.5, "BET_P": 0.5},
+    domain=(9, 6, 160),
+)(vertical_advection_dycore)
+
+
 def section_gap_register_temp(a: F64, out: F64):
     """A register-only temporary read two levels down across a gap between sections (the gap
     level never runs; the value must survive it)."""

@@ -101,7 +101,8 @@ def test_golden_case(name):
 # split cached/uncached writer segments, no tail cache at all, a shallow load ring
 COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tail_bwd_fwd", "tail_bwd_fwd_short",
                     "tail_fwd_bwd_offsets", "tridiag", "tridiag_k161", "tridiag_k2", "tridiag_k70",
-                    "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80"]
+                    "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80",
+                    "vertical_advection_dycore_k160"]
 COLUMN_OPTS = [{"kreg": 32}, {"kreg": 16, "seg_tail": 1}, {"seg_tail": 1}, {"ktail_lds": 0}, {"kring": 3},
                {"kreg": 96}, {"kreg": 64, "kreg_pf": 0}, {"kreg": 48, "kreg_pf": 3}]
 
@@ -266,6 +267,31 @@ def test_hdiff_bufld_strips_vs_c_oracle(opts, dtype, ni, nj):
     ref = np.full((ni + 3, nj + 2, nk), -7.0, dtype=dtype, order="F")
     c_oracle.horizontal_diffusion(np.asfortranarray(in_h), ref, np.asfortranarray(co_h), org, (ni, nj, nk))
     gu.assert_match(storage.to_numpy(out_d), ref, name=f"hdiff_bufld_{ni}x{nj}")
+
+
+def test_vadv_register_band_vs_numpy_backend():
+    """vadv with the default column kernel (auto register band of 96 levels, band
+    fronts prefetched; LDS tail below it; scratch for the rest) over several ragged column blocks,
+    bit-exact against the numpy backend (itself pinned to the reference goldens), plus the short
+    column (nk < the band's minimum) that runs the same library without the band."""
+    _torch()
+    import bench
+    from gt4py_amd import gtscript, storage
+
+    defn = bench.stencil_defs()[("vertical_advection_dycore", np.float64)]
+    ext = bench.EXTERNALS["vertical_advection_dycore"]
+    gpu = gtscript.stencil(backend=BACKEND, definition=defn, name="parity.vadv_band", externals=ext)
+    assert "regband" in gpu._gt_run_impl_.compiled.source
+    cpu = gtscript.stencil(backend="numpy", definition=defn, name="parity.vadv_band.np", externals=ext)
+    for ni, nj, nk in ((133, 37, 160), (70, 9, 96)):
+        rng = np.random.default_rng(ni + nk)
+        host = {n: rng.uniform(-1, 1, (ni, nj, nk)) for n in ("utens_stage", "u_stage", "u_pos", "utens")}
+        host["wcon"] = rng.uniform(-1, 1, (ni + 1, nj, nk + 1))
+        ref = {k: v.copy() for k, v in host.items()}
+        cpu(**ref, dtr_stage=0.15, origin=(0, 0, 0), domain=(ni, nj, nk))
+        dev = {k: storage.from_array(v, backend=BACKEND) for k, v in host.items()}
+        gpu(**dev, dtr_stage=0.15, origin=(0, 0, 0), domain=(ni, nj, nk))
+        gu.assert_match(storage.to_numpy(dev["utens_stage"]), ref["utens_stage"], name=f"vadv {ni}x{nj}x{nk}")
 
 
 def test_outside_domain_untouched():
