@@ -452,22 +452,24 @@ def box_identity(dev_index: int = 0):
 # ------------------------------------------------------------------------------------------
 
 
-def hbm_estimate(cfg, domain, args, candidates) -> dict:
+def hbm_estimate(stencil, args, candidates) -> dict:
     """Peak device memory of one rank for this config (bytes, from the allocated fields): the
-    fields themselves, the placement tuner's transient copies of the written fields (a backup plus
-    ``candidates`` buffer sets, each padded by 2 MiB; the tuner itself caps the sets at 80 % of
-    free memory) and the halo path's pack buffers (small). DESIGN.md §6."""
-    try:
-        fields = sum(t.untyped_storage().nbytes() for t in args)
-    except AttributeError:  # dry run on host arrays
-        fields = sum(getattr(t, "nbytes", 0) for t in args)
-    sname, dtype, _, _, _ = CONFIGS[cfg]
-    ni, nj, nk = domain
-    item = np.dtype(dtype).itemsize
-    written = {"horizontal_diffusion": 1, "horizontal_diffusion_blocks": 1, "lap5": 1, "copy_stencil": 1,
-               "tridiagonal_solver": 3, "vertical_advection_dycore": 1, "staged_forward_ij_temp": 1}.get(sname, 1)
-    per_written = (ni + 32) * nj * nk * item + (2 << 20)
-    tuner = (1 + candidates) * written * per_written if candidates > 0 else 0
+    fields themselves, and the placement tuner's transient copies of the fields the stencil writes
+    (a backup plus ``candidates`` buffer sets, each padded by 2 MiB; the tuner itself caps the sets
+    at 80 % of free memory); the halo path's pack buffers are faces, negligible. DESIGN.md §6."""
+    from gt4py_amd.storage.placement import written_fields
+
+    def nbytes(t):
+        try:
+            return t.untyped_storage().nbytes()
+        except AttributeError:  # dry run on host arrays
+            return getattr(t, "nbytes", 0)
+
+    names = list(stencil.field_info)
+    fields = sum(nbytes(t) for t in args)
+    written = set(written_fields(stencil))
+    per_set = sum(nbytes(t) + (2 << 20) for n, t in zip(names, args) if n in written)
+    tuner = (1 + candidates) * per_set if candidates > 0 else 0
     return {"fields_gb": round(fields / 1e9, 6), "tuner_transient_gb": round(tuner / 1e9, 6),
             "peak_gb": round((fields + tuner) / 1e9, 6)}
 
@@ -582,7 +584,7 @@ class Workload:
         self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain)
         self.placement = None
         self.untuned = None
-        self.hbm_estimate = hbm_estimate(cfg, self.domain, self.args, getattr(args, "placement_candidates", 0))
+        self.hbm_estimate = hbm_estimate(self.stencil, self.args, getattr(args, "placement_candidates", 0))
         ncand = getattr(args, "placement_candidates", 0)
         if not dry_run and ncand > 0:
             self.tune_placement(ncand, args)
