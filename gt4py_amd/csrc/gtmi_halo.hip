@@ -22,7 +22,8 @@ static thread_local char g_err[512];
 
 // A box is ej*ek ROWS of ei elements contiguous along I (the field's I stride) and along the
 // buffer. Narrow boxes (the I faces of a 2-D exchange: ei = halo width, one or two 8-B cells per
-// row) take one row per lane, so a wave touches 64 rows with no index math per element; wide
+// row) take one 16-B row per lane when the face row is 16 B and aligned, else one element per
+// lane with 32-bit index math (the lanes of a row share its line; the buffer side is contiguous); wide
 // boxes (J faces: whole rows) take 64-element chunks of a row per wave, coalesced along I. Row and
 // chunk indices are computed once per lane (narrow, 32-bit when the box allows) or once per wave
 // in scalar registers (wide), not per element: the round-2 kernel's three 64-bit divisions per
@@ -52,22 +53,41 @@ __device__ __forceinline__ void copy_box(const gtmi_box& bx, int direction) {
     if (ei <= 0 || rows <= 0) return;
     if (ei <= GTMI_HALO_NARROW) {
         const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-        int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (rows <= 0xffffffffLL && ej <= 0xffffffffLL) {  // 32-bit row -> (j, k)
+        const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int64_t si = bx.strides[0], sj = bx.strides[1], sk = bx.strides[2];
+        const int64_t base = bx.start[0] * si + bx.start[1] * sj + bx.start[2] * sk;
+        // a 16-B face row (two 8-B or four 4-B cells) moved as ONE 16-B access per lane: the
+        // lanes of a wave then fill 1 KB of the buffer contiguously
+        const bool vec16 = ei * (int64_t)sizeof(T) == 16 && si == 1 &&
+                           ((uintptr_t)((T*)bx.field + base) % 16) == 0 && (sj * (int64_t)sizeof(T)) % 16 == 0 &&
+                           (sk * (int64_t)sizeof(T)) % 16 == 0 && ((uintptr_t)bx.buffer % 16) == 0;
+        if (vec16 && rows <= 0xffffffffLL) {
             const uint32_t uej = (uint32_t)ej;
-            for (; r < rows; r += nthreads) {
+            for (int64_t r = t0; r < rows; r += nthreads) {
                 const uint32_t ur = (uint32_t)r, j = ur % uej, k = ur / uej;
-                T* __restrict__ f = (T*)bx.field + ((bx.start[1] + j) * bx.strides[1] + (bx.start[2] + k) * bx.strides[2] +
-                                                    bx.start[0] * bx.strides[0]);
-                T* __restrict__ buf = (T*)bx.buffer + r * ei;
-                if (direction == 0) {
-                    for (int64_t i = 0; i < ei; ++i) buf[i] = f[i * bx.strides[0]];
-                } else {
-                    for (int64_t i = 0; i < ei; ++i) f[i * bx.strides[0]] = buf[i];
-                }
+                ulonglong2* f = (ulonglong2*)((T*)bx.field + base + (int64_t)j * sj + (int64_t)k * sk);
+                ulonglong2* b = (ulonglong2*)bx.buffer + r;
+                if (direction == 0)
+                    *b = *f;
+                else
+                    *f = *b;
+            }
+            return;
+        }
+        const int64_t n = rows * ei;  // one element per lane: lanes of a row share its line
+        if (n <= 0xffffffffLL) {
+            const uint32_t uei = (uint32_t)ei, uej = (uint32_t)ej;
+            for (int64_t e = t0; e < n; e += nthreads) {
+                const uint32_t ue = (uint32_t)e, r = ue / uei, i = ue - r * uei, j = r % uej, k = r / uej;
+                T* f = (T*)bx.field + base + (int64_t)i * si + (int64_t)j * sj + (int64_t)k * sk;
+                T* b = (T*)bx.buffer + e;
+                if (direction == 0)
+                    *b = *f;
+                else
+                    *f = *b;
             }
         } else {
-            for (; r < rows; r += nthreads) copy_row<T>(bx, r, 0, ei, direction, 1);
+            for (int64_t r = t0; r < rows; r += nthreads) copy_row<T>(bx, r, 0, ei, direction, 1);
         }
         return;
     }
@@ -138,7 +158,7 @@ static int halo_copy_impl(const gtmi_box* boxes, int32_t n_boxes, int32_t direct
         int64_t units = 0;
         for (int b = 0; b < nb; ++b) {
             const int64_t ei = lb.b[b].extent[0], rows = lb.b[b].extent[1] * lb.b[b].extent[2];
-            const int64_t lanes = ei <= GTMI_HALO_NARROW ? rows : rows * ((ei + 63) / 64) * 64;
+            const int64_t lanes = ei <= GTMI_HALO_NARROW ? rows * ei : rows * ((ei + 63) / 64) * 64;
             if (lanes > units) units = lanes;
         }
         int64_t blocks = (units + 255) / 256;

@@ -447,3 +447,36 @@ def test_batched_halo_copy_roundtrip():
     for (t, s, e), t2 in zip(boxes, (a2, a2, b2)):
         sl = (slice(s[0], s[0] + e[0]), slice(s[1], s[1] + e[1]), slice(s[2], s[2] + e[2]))
         assert torch.equal(t2[sl], t[sl])
+
+
+@pytest.mark.parametrize("dtype,ei,i0", [("float64", 2, 2), ("float64", 2, 3), ("float32", 4, 4),
+                                          ("float32", 2, 1), ("float64", 3, 0), ("float64", 1, 5)])
+def test_batched_halo_copy_narrow_faces(dtype, ei, i0):
+    """I faces of the 2-D exchange (a few cells per row of an I-first field): the 16-B row path
+    (aligned 16-B face rows) and the element path (other widths / alignments), pack and unpack."""
+    torch = _torch()
+    from gt4py_amd import storage
+    from gt4py_amd.distributed.halo_copy import BatchedCopy
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(ei * 10 + i0)
+    t = storage.empty((40, 23, 5), np.dtype(dtype), backend=BACKEND, aligned_index=(0, 0, 0))
+    t.copy_(torch.rand(t.shape, generator=g, device=dev, dtype=t.dtype))
+    boxes = [(t, (i0, 0, 0), (ei, 23, 5)), (t, (40 - ei, 1, 1), (ei, 21, 4))]
+    bufs = [torch.empty(e[0] * e[1] * e[2], dtype=t.dtype, device=dev) for _, _, e in boxes]
+    BatchedCopy([(f, s, e, b) for (f, s, e), b in zip(boxes, bufs)]).run(0)
+    torch.cuda.synchronize()
+    for (f, s, e), b in zip(boxes, bufs):
+        ref = f[s[0]:s[0] + e[0], s[1]:s[1] + e[1], s[2]:s[2] + e[2]].permute(2, 1, 0).reshape(-1)
+        assert torch.equal(b, ref)
+    t2 = storage.zeros((40, 23, 5), np.dtype(dtype), backend=BACKEND, aligned_index=(0, 0, 0))
+    BatchedCopy([(t2, s, e, b) for (_, s, e), b in zip(boxes, bufs)]).run(1)
+    torch.cuda.synchronize()
+    for _, s, e in boxes:
+        sl = (slice(s[0], s[0] + e[0]), slice(s[1], s[1] + e[1]), slice(s[2], s[2] + e[2]))
+        assert torch.equal(t2[sl], t[sl])
+    mask = torch.ones_like(t2, dtype=torch.bool)
+    for _, s, e in boxes:
+        mask[s[0]:s[0] + e[0], s[1]:s[1] + e[1], s[2]:s[2] + e[2]] = False
+    assert float(t2[mask].abs().sum()) == 0.0  # nothing outside the boxes written
