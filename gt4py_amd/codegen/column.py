@@ -842,7 +842,9 @@ class ColumnGen:
                 # of their own (a level waiting for its own loads stalls a one-wave-per-SIMD kernel)
                 order_us = sorted(us, reverse=not fwd)
                 kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
-                Pb = int(self.opts.get("kreg_pf", P))
+                # default: 4 levels deeper than the load ring (vadv 1024^2x160, kreg 96: pf 8 1.854,
+                # 12 1.822, 16 1.914, 24 2.159 ms; profiles/r04/sweep_vadv_band_pf.log)
+                Pb = int(self.opts.get("kreg_pf", P + 4))
                 mem_keys = {}
                 for u in order_us:
                     mk = []
