@@ -599,8 +599,16 @@ class Workload:
         steps, warm = (args.steps, args.warmup) if self.cfg == args.config else (args.extra_steps, 3)
         el, km = time_workload(self, steps, warm, self.dev, None, step=self.plain_step)
         self.untuned = {"ms_per_step": el / steps * 1e3, "kernel_ms": km}
-        self.placement = self.stencil.tune_placement(*self.args, **self.params, origin=self.origin,
-                                                     domain=self.domain, candidates=candidates)
+        try:
+            self.placement = self.stencil.tune_placement(*self.args, **self.params, origin=self.origin,
+                                                         domain=self.domain, candidates=candidates)
+        except (ValueError, RuntimeError, TypeError) as e:
+            # a refusal (e.g. a viewed or weakly referenced written field) leaves the first
+            # allocation in place: the line then reports the untuned figure as the headline
+            import torch
+
+            torch.cuda.synchronize()
+            self.placement = {"error": f"{type(e).__name__}: {e}"[:300], "in_place": False}
 
     def step(self):
         if self.halo is not None:
@@ -723,8 +731,8 @@ def sharded_leg(cfg, args, rank, world, dev, backend, dist) -> dict:
                 "of this config is the single-GPU reference for weak-scaling efficiency",
     }
     if w.placement is not None:
-        rec["placement_untuned_ms"] = w.placement["untuned_ms"]
-        rec["placement_tuned_ms"] = w.placement["tuned_ms"]
+        rec["placement_untuned_ms"] = w.placement.get("untuned_ms")
+        rec["placement_tuned_ms"] = w.placement.get("tuned_ms")
     del w
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -1066,7 +1074,8 @@ def main():
                     "library": w.library_key(),
                 }
                 if w.placement is not None:
-                    extra[cfg]["placement"] = {k: w.placement[k] for k in ("candidates_ms", "chosen", "untuned_ms")}
+                    extra[cfg]["placement"] = {k: w.placement.get(k) for k in ("candidates_ms", "chosen", "untuned_ms",
+                                                                               "error") if k in w.placement}
                 if w.untuned is not None and w.untuned["kernel_ms"]:
                     u_gbs = n_i * n_j * n_k * w.bpc / (w.untuned["kernel_ms"] * 1e-3) / 1e9
                     extra[cfg]["kernel_ms_untuned"] = round(w.untuned["kernel_ms"], 4)
