@@ -74,7 +74,7 @@ def main():
         lambda: st(fin, out, coeff, origin=origin, domain=dom, validate_args=False), args.calls)
     frozen = st.freeze(origin=origin, domain=dom)
     res["frozen"] = timeit(lambda: frozen(in_field=fin, out_field=out, coeff=coeff), args.calls)
-    (entry,) = type(st)._gt_fast_memo_.values()
+    ((entry,),) = type(st)._gt_fast_memo_.values()  # one argument tuple, one (domain, origin) signature
     prepared = entry[2]  # what the cached __call__ ends in (native Prepared, or the ctypes closure)
     print(json.dumps({"prepared_kind": type(prepared).__name__}), flush=True)
     res["prepared_only"] = timeit(lambda: prepared((fin, out, coeff), ()), args.calls)
