@@ -38,7 +38,9 @@ LDS_BYTES = 160 * 1024  # per CU (MI355X_MICROARCH.md); one 256-thread block may
 DEFAULT_RING = 8
 # register band levels (option ``kreg``; -1 = auto, see ColumnGen._plan_register_band)
 DEFAULT_KREG = -1
-AUTO_KREG = 96
+AUTO_KREG = 96  # write-free scratch tails
+AUTO_KREG_API = 48  # tails of API outputs
+AUTO_KREG_API_PF = 6
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -97,6 +99,7 @@ class ColumnGen:
                 raise ValueError(f"tile_ti must be in [8, {bx - ilo - ihi}] for IJ extent {self.ext}, got {ti}")
         self.info = {li: self._analyse_loop(li) for li in kernel.loops}
         self.kreg = 0
+        self.band_pf_default = None
         self.tail = None if self.tile else self._plan_tail()
 
     def _mem(self, name):
@@ -275,6 +278,7 @@ class ColumnGen:
         level's section must be known statically: true for ``nk >= band_nmin`` (checked at run time;
         below it the kernel runs without the register band)."""
         self.kreg = 0
+        self.band_pf_default = None
         R = int(self.opts.get("kreg", DEFAULT_KREG))
         if R < 0:
             # auto: a band of AUTO_KREG levels when every cached field is a scratch temporary that
@@ -284,8 +288,18 @@ class ColumnGen:
             # 64: 2.00, 112: 1.94 ms). When the cached fields are API outputs (tridiag's sup/rhs,
             # written anyway) the band saves only the re-read and costs more than it saves
             # (kreg 32: -1.3 %, 64: +5 %, 96: +35 %), so no band (profiles/r04/r04c_sweep_*_kreg.log)
+            # Cached API outputs (tridiag's sup/rhs, written at every level anyway): the band saves
+            # only the re-read; a moderate band with a shallow prefetch still pays a little
+            # (tridiag 1024^2x160: kreg 48 / pf 6 1.826 ms vs 1.869 without; 16: 1.851, 32: 1.841;
+            # 64 and beyond lose, profiles/r04/r04h_sweep_tridiag_band.log)
             per_level = sum(self.st.decl(n).dtype.itemsize for n in t.fields)
-            R = AUTO_KREG if (t.fields and all(n in t.no_store for n in t.fields) and per_level <= 16) else 0
+            if not t.fields or per_level > 16:
+                R = 0
+            elif all(n in t.no_store for n in t.fields):
+                R = AUTO_KREG
+            else:
+                R = AUTO_KREG_API
+                self.band_pf_default = AUTO_KREG_API_PF
         if R <= 0:
             return
         B = self.info[t.b]
@@ -844,7 +858,7 @@ class ColumnGen:
                 kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
                 # default: 4 levels deeper than the load ring (vadv 1024^2x160, kreg 96: pf 8 1.854,
                 # 12 1.822, 16 1.914, 24 2.159 ms; profiles/r04/sweep_vadv_band_pf.log)
-                Pb = int(self.opts.get("kreg_pf", P + 4))
+                Pb = int(self.opts.get("kreg_pf", self.band_pf_default if self.band_pf_default is not None else P + 4))
                 mem_keys = {}
                 for u in order_us:
                     mk = []
