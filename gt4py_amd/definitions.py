@@ -155,3 +155,18 @@ def filter_mask(seq, mask):
 def interpolate_mask(seq, mask, default):
     it = iter(seq)
     return tuple(next(it) if m else default for m in mask)
+
+
+# Error hierarchy of the reference (``src/gt4py/cartesian/definitions.py:152-165``): frontend
+# errors derive from these, so ``except GTError`` / ``except GTSyntaxError`` catch the same
+# errors as with the reference.
+class GTError(Exception):
+    pass
+
+
+class GTSyntaxError(GTError):
+    pass
+
+
+class GTSpecificationError(GTError):
+    pass

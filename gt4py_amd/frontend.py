@@ -26,6 +26,7 @@ import builtins
 import inspect
 import itertools
 import numbers
+import sys
 import textwrap
 import types
 from typing import Any, Dict, List, Optional, Tuple
@@ -34,21 +35,44 @@ import numpy as np
 
 from gt4py_amd import ir
 from gt4py_amd.gtscript import Axis
+from gt4py_amd.definitions import GTSpecificationError, GTSyntaxError
 from gt4py_amd.ir import DataType
 
 _GTSCRIPT_FUNC_ATTR = "__gtscript_function__"
 
 
-class GTScriptSyntaxError(SyntaxError):
+# the reference's frontend error hierarchy (``frontend/exceptions.py:15-100``): symbol and
+# definition errors ARE syntax errors, assertion failures are specification errors
+class GTScriptSyntaxError(GTSyntaxError):
     pass
 
 
-class GTScriptSymbolError(NameError):
+class GTScriptSymbolError(GTScriptSyntaxError):
     pass
 
 
-class GTScriptDefinitionError(ValueError):
+class GTScriptDefinitionError(GTScriptSyntaxError):
     pass
+
+
+class GTScriptValueError(GTScriptDefinitionError):
+    pass
+
+
+class GTScriptDataTypeError(GTScriptSyntaxError):
+    pass
+
+
+class GTScriptAssertionError(GTSpecificationError):
+    pass
+
+
+def _valid_external(value) -> bool:
+    """An external's value the reference accepts (``GTScriptParser.CONST_VALUE_TYPES``: numbers,
+    bools, numpy scalars, functions, None, axis indices and axes)."""
+    from gt4py_amd.gtscript import AxisIndex
+
+    return value is None or isinstance(value, (bool, numbers.Number, np.generic, types.FunctionType, AxisIndex, Axis))
 
 
 def annotate_function(func):
@@ -283,6 +307,18 @@ class StencilParser:
         return ir.LoopOrder(int(val))
 
     def _parse_interval(self, node, scope) -> ir.Interval:
+        """``interval(start, end)`` with the reference's range checks (``gtscript_frontend.py:
+        1105-1140``, ``IntervalParser``): no ``None`` start, no END-relative start with a
+        START-relative end, and a non-empty range when both ends are relative to the same level."""
+        itv = self._parse_interval_bounds(node, scope)
+        where = f"at line {node.lineno} (column {node.col_offset + 1})"
+        s_, e_ = itv.start, itv.end
+        if (s_.level == ir.LevelMarker.END and e_.level == ir.LevelMarker.START) or (
+                s_.level == e_.level and e_.offset <= s_.offset):
+            raise GTScriptSyntaxError(f"Invalid interval range specification {where}")
+        return itv
+
+    def _parse_interval_bounds(self, node, scope) -> ir.Interval:
         args = node.args
         if len(args) == 1 and isinstance(args[0], ast.Constant) and args[0].value is Ellipsis:
             return ir.Interval(ir.AxisBound(ir.LevelMarker.START, 0), ir.AxisBound(ir.LevelMarker.END, 0))
@@ -294,7 +330,10 @@ class StencilParser:
 
         def bound(a, is_start):
             if isinstance(a, ast.Constant) and a.value is None:
-                return ir.AxisBound(ir.LevelMarker.START if is_start else ir.LevelMarker.END, 0)
+                if is_start:  # the reference's IntervalParser refuses a None start
+                    raise GTScriptSyntaxError(
+                        f"Invalid interval range specification at line {node.lineno} (column: {node.col_offset + 1})")
+                return ir.AxisBound(ir.LevelMarker.END, 0)
             runtime = [
                 n.id for n in ast.walk(a)
                 if isinstance(n, ast.Name) and n.id not in scope.imported
@@ -314,7 +353,10 @@ class StencilParser:
                 level = ir.LevelMarker.START if v.index >= 0 else ir.LevelMarker.END
                 return ir.AxisBound(level, v.index + v.offset)
             if v is None:
-                return ir.AxisBound(ir.LevelMarker.START if is_start else ir.LevelMarker.END, 0)
+                if is_start:
+                    raise GTScriptSyntaxError(
+                        f"Invalid interval range specification at line {node.lineno} (column: {node.col_offset + 1})")
+                return ir.AxisBound(ir.LevelMarker.END, 0)
             v = int(v)
             if v < 0:
                 return ir.AxisBound(ir.LevelMarker.END, v)
@@ -352,8 +394,23 @@ class StencilParser:
 
         def key(sec):
             b = sec.interval.start
-            return (0 if b.level == ir.LevelMarker.START else 1, b.offset)
+            return (0 if b.level == ir.LevelMarker.START else 100000) + b.offset
 
+        if len(items) == 1 and sections:
+            # nested intervals: listed in execution order and disjoint (gtscript_frontend.py:
+            # 1019-1079, 1996-2004)
+            where = (f"Invalid 'with' statement in '{self.definition.__name__}' at line {stmt.lineno} "
+                     f"(column {stmt.col_offset + 1})")
+            if sorted(sections, key=key, reverse=(order == ir.LoopOrder.BACKWARD)) != sections:
+                raise GTScriptSyntaxError(f"{where}: Intervals must be specified in order of execution.")
+
+            def pos(b):
+                return b.offset if b.level == ir.LevelMarker.START else sys.maxsize + b.offset
+
+            for a, b in zip(sections, sections[1:]):
+                a0, a1, b0, b1 = pos(a.interval.start), pos(a.interval.end), pos(b.interval.start), pos(b.interval.end)
+                if (b0 <= a0 < b1) or (a0 <= b0 < a1):
+                    raise GTScriptSyntaxError(f"{where}: Overlapping intervals detected.")
         sections.sort(key=key, reverse=(order == ir.LoopOrder.BACKWARD))
         # drop empty sections (e.g. everything inlined away)
         sections = [s for s in sections if s.body]
@@ -377,7 +434,8 @@ class StencilParser:
                 return []
             if isinstance(s.value, ast.Call) and self._call_name(s.value) == "compile_assert":
                 if not self._const_eval(s.value.args[0], scope):
-                    raise GTScriptDefinitionError(f"compile_assert failed (line {s.lineno})")
+                    raise GTScriptAssertionError(f"Assertion failed at line {s.lineno}, col {s.col_offset + 1}:\n"
+                                                 f"{ast.unparse(s.value.args[0])}")
                 return []
             raise GTScriptSyntaxError(f"Invalid expression statement (line {s.lineno})")
         if isinstance(s, ast.Pass):
@@ -465,7 +523,8 @@ class StencilParser:
                 return [ir.HorizontalRegion([m], body if n == 0 else copy.deepcopy(body)) for n, m in enumerate(masks)]
             raise GTScriptSyntaxError(f"Invalid 'with' statement inside a computation (line {s.lineno})")
         if isinstance(s, ast.Return):
-            raise GTScriptSyntaxError("'return' is only allowed in gtscript functions")
+            # the reference refuses it while building its IR with a ValueError (not a GTScript error)
+            raise ValueError("'return' is only allowed in gtscript functions")
         raise GTScriptSyntaxError(f"Unsupported statement {type(s).__name__} (line {getattr(s, 'lineno', '?')})")
 
     def _parse_region(self, node, scope) -> ir.HorizontalMask:
@@ -676,6 +735,14 @@ class StencilParser:
                 if t_didx:
                     raise GTScriptSyntaxError("Temporaries with data dimensions need to be declared explicitly.")
                 self.temporaries[name_res] = ir.FieldDecl(name_res, DataType.AUTO, is_temporary=True)
+        decl = self.fields.get(name_res) or self.temporaries.get(name_res)
+        axes = tuple(getattr(decl, "axes", ("I", "J", "K")) or ("I", "J", "K"))
+        need = ["I", "J"] + (["K"] if getattr(self, "_loop_order", None) == ir.LoopOrder.PARALLEL else [])
+        if set(need) - set(axes):
+            # a lower-dimensional field is written only by a sweep that covers its missing axes
+            # (reference gtscript_frontend.py:1894-1902)
+            raise GTScriptSyntaxError(
+                f"Cannot assign to field '{name}' as all parallel axes '{need}' are not present.")
         if t_off != (0, 0, 0) or t_didx:
             tgt = self._field_access(name_res, t_off, scope, t_didx)
             if tgt.offset[2] != 0 or tgt.k_offset is not None:
@@ -702,6 +769,7 @@ class StencilParser:
         )
         if axis_form:
             off = [0, 0, 0]
+            last = -1  # axes in I, J, K order, each once (reference gtscript_frontend.py:1326-1339)
             for e in elts:
                 shift = 0
                 node = e
@@ -711,7 +779,13 @@ class StencilParser:
                 ax = self._try_const(node, scope)
                 if not isinstance(ax, Axis):
                     raise GTScriptSyntaxError("Invalid axis offset expression")
-                off["IJK".index(ax.name)] = shift
+                idx = "IJK".index(ax.name)
+                if idx < last:
+                    raise GTScriptSyntaxError(f"Axis {ax.name} is specified out of order")
+                if idx == last:
+                    raise GTScriptSyntaxError(f"Duplicate axis found: {ax.name}")
+                last = idx
+                off[idx] = shift
             return ("axes", tuple(off))
         vals = []
         for e in elts:
@@ -819,6 +893,9 @@ class StencilParser:
                     raise GTScriptSyntaxError(f"Offset access to constant '{name}'")
                 self.used_externals.setdefault(name, val)
                 return self._literal(val)
+            if name in scope.imported and not _valid_external(val):
+                # the reference's GTScriptParser.eval_external (gtscript_frontend.py:2317-2334)
+                raise GTScriptDefinitionError(f"Missing or invalid value for external symbol {name}")
         raise GTScriptSymbolError(f"Unknown symbol '{name}'")
 
     def _parse_expr(self, node, scope: _Scope, pre: List[ir.Stmt]) -> ir.Expr:
@@ -939,7 +1016,18 @@ class StencilParser:
             if not found:
                 raise GTScriptSymbolError(f"Unknown function '{node.func.id}'")
         elif isinstance(node.func, ast.Attribute):
-            func_obj = self._const_eval(node.func, scope)
+            # a dotted callee is an external symbol to the reference (``np.sqrt``, ``gtscript.sqrt``):
+            # its value must be a gtscript function (eval_external + resolve_external_symbols,
+            # gtscript_frontend.py:2317-2354)
+            dotted = ast.unparse(node.func)
+            try:
+                func_obj = self._const_eval(node.func, scope)
+            except Exception as ex:  # noqa: BLE001
+                raise GTScriptDefinitionError(f"Missing or invalid value for external symbol {dotted}") from ex
+            if not is_gtscript_function(func_obj):
+                if isinstance(func_obj, types.FunctionType):
+                    raise TypeError(f"{func_obj.__name__} is not a gtscript function")
+                raise GTScriptDefinitionError(f"Missing or invalid value for external symbol {dotted}")
         if is_gtscript_function(func_obj):
             (res,) = self._inline_call(node, scope, pre, n_results=1, func=func_obj)
             return res

@@ -209,18 +209,20 @@ def test_no_write_and_read_with_horizontal_offset(backend):
 def test_temporary_declared_in_definition_order(backend):
     """A temporary belongs to the interval block that assigns it FIRST IN THE DEFINITION
     (gtc/gtir.py:226-240: each block is a GTIR VerticalLoop with its own ``temporaries``),
-    not to the block that comes first in the sweep: here ``tmp`` is declared by the upper block,
-    so the lower block, defined later, writes it and reads it at an I offset -- rejected."""
+    whatever the statements of a later block do: here ``tmp`` is declared by the lower block, so
+    the upper block, defined later, writes it and reads it at an I offset -- rejected (checked
+    against the reference itself; blocks must also be listed in execution order, which the
+    reference enforces first, tests/frontend_cases.py)."""
     with pytest.raises(ValueError, match="Illegal write and read with horizontal offset"):
 
         @gtscript.stencil(backend=backend)
         def declared_later(a: Field[np.float64], b: Field[np.float64]) -> None:
             with computation(PARALLEL):
-                with interval(1, None):
-                    tmp = a * 2
-                    b = tmp
                 with interval(0, 1):
                     tmp = a
+                    b = tmp
+                with interval(1, None):
+                    tmp = a * 2
                     b = tmp[1, 0, 0]
 
     # defined the other way round the lower block declares tmp and may read it at an offset
