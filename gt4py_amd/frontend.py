@@ -483,6 +483,10 @@ class StencilParser:
                 return self._parse_block(s.body if cond else s.orelse, scope)
             pre: List[ir.Stmt] = []
             cond = self._parse_expr(s.test, scope, pre)
+            if pre or self._calls_gtscript_function(s.test, scope):  # gtscript_frontend.py:1607-1616
+                raise GTScriptSyntaxError(
+                    "Using function calls in the condition of an if is not allowed, the function needs to be "
+                    f"assigned to a variable outside the condition (line {s.lineno})")
             body = self._parse_block(s.body, scope)
             orelse = self._parse_block(s.orelse, scope)
             return pre + [ir.If(cond, body, orelse)]
@@ -884,8 +888,10 @@ class StencilParser:
         if name in ("True", "False"):
             return ir.Literal(name == "True", DataType.BOOL)
         if name in ("I", "J", "K") and not any(offset):
-            # iterator access: the current index along an axis (gtir.IteratorAccess)
-            return ir.AxisIndex("IJK".index(name))
+            # iterator access (gtir.IteratorAccess): only K may be queried (gtscript_frontend.py:860-872)
+            if name != "K":
+                raise GTScriptSyntaxError(f"Parallel axis {name} can't be queried - only K")
+            return ir.AxisIndex(2)
         found, val = scope.lookup_external(name)
         if found:
             if isinstance(val, (bool, np.bool_, numbers.Number, np.generic)):
@@ -1056,6 +1062,15 @@ class StencilParser:
         return ir.NativeCall(native, args)
 
     # ------------------------------------------------------------------ inlining
+    def _calls_gtscript_function(self, expr: ast.AST, scope: _Scope) -> bool:
+        """Whether ``expr`` calls a gtscript function (native functions excluded)."""
+        for n in ast.walk(expr):
+            if isinstance(n, ast.Call) and isinstance(n.func, ast.Name):
+                found, func = scope.lookup_external(n.func.id)
+                if found and is_gtscript_function(func):
+                    return True
+        return False
+
     def _inline_call(self, node: ast.Call, scope: _Scope, pre: List[ir.Stmt], n_results: int, func=None):
         if func is None:
             if isinstance(node.func, ast.Name):

@@ -27,7 +27,13 @@ from gt4py_amd.gtscript import (
     computation,
     horizontal,
     interval,
+    asin,
+    cos,
+    float32,
+    float64,
+    isfinite,
     region,
+    sin,
 )
 
 F64 = Field[np.float64]
@@ -448,3 +454,176 @@ def ext_module_value(a: F64, b: F64):
 def lowdim_k_write(a: F64, b: Field[gtscript.K, np.float64]):
     with computation(FORWARD), interval(...):
         b = a
+
+
+# ----------------------------------------------------------------------------- native functions,
+# absolute K indexing, casts, typed temporaries, the K iterator (cf. the reference's
+# TestNativeFunctions, TestFunctionIfError, TestAbsoluteIndex, TestLiteralCasts,
+# TestTemporaryTypes, TestNumpyTypedConstants, TestIteratorAccess)
+
+NP_F32_CONST = np.float32(42.0)
+
+
+@gtscript.function
+def _boolean_return(x):
+    return x == 1.0
+
+
+@gtscript.function
+def _sinus(x):
+    return sin(x)
+
+
+@case()
+def native_offset_arg_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = sin(a[1, 0, 0]) + cos(a)
+
+
+@case()
+def native_nested_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = min(abs(sin(a)), -0.5)  # the Python builtins' names, as the reference's own test
+
+
+@case()
+def native_in_function_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = _sinus(a) + 1.0
+
+
+@case()
+def native_not_isfinite_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = not isfinite(a)
+
+
+@case()
+def native_ternary_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = asin(a) + 1 if 1 < a else sin(a)
+
+
+@case()
+def native_dotted(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = gtscript.sin(a)
+
+
+@case()
+def native_wrong_arity(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = sin(a, a)
+
+
+@case()
+def function_call_in_if(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = 0.0
+        if _boolean_return(a):
+            b = 1.0
+
+
+@case()
+def abs_k_positional(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a.at(2)
+
+
+@case()
+def abs_k_with_i(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a.at(I=1, K=0)
+
+
+@case()
+def abs_k_iterator(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a.at(K=K)
+
+
+@case()
+def literal_casts_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(0, 1):
+        b = float(0) + int(3) + a
+
+
+@case()
+def typed_temporaries_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        t32: float32 = 12.12
+        t64: float64 = 34.34
+        ti: int = 12
+        b = t32 + t64 + ti + a
+
+
+@case()
+def numpy_typed_constant_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a + NP_F32_CONST
+
+
+@case()
+def k_iterator_read_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a + K
+
+
+@case()
+def k_iterator_condition_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a
+        if K == 2:
+            b = 42.0
+
+
+@case()
+def i_iterator_condition(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a
+        if I == 2:
+            b = 42.0
+
+
+@case()
+def while_loop_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        t = a
+        while t < 10.0:
+            t = t + 1.0
+        b = t
+
+
+@case()
+def if_elif_else_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        if a > 1.0:
+            b = 1.0
+        elif a > 0.0:
+            b = 2.0
+        else:
+            b = 3.0
+
+
+@case()
+def bool_ops_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = 1.0 if (a > 0.0 and a < 1.0) or not (a == 2.0) else 0.0
+
+
+@case()
+def power_ok(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = a**2 + a**0.5
+
+
+@case()
+def unsupported_lambda(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = (lambda x: x)(a)
+
+
+@case()
+def unsupported_list(a: F64, b: F64):
+    with computation(PARALLEL), interval(...):
+        b = [a, a][0]
