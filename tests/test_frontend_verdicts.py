@@ -99,7 +99,8 @@ def test_accepted_case_results_gpu(name):
     defn, externals = fc.CASES[name]
     ins, org, par, want = case_io(name)
     st = gtscript.stencil(backend="gt:mi355x", definition=defn, externals=externals, name=f"verdict.gpu.{name}")
-    dev = {k: storage.from_array(v, None, backend="gt:mi355x", aligned_index=org[k]) for k, v in ins.items()}
+    dev = {k: storage.from_array(v, None, backend="gt:mi355x", aligned_index=org[k] + (0,) * (v.ndim - len(org[k])))
+           for k, v in ins.items()}
     st(**dev, **par, origin=org, domain=DOMAIN)
     for k, v in want.items():
         got = storage.to_numpy(dev[k])
