@@ -41,6 +41,12 @@ DEFAULT_KREG = -1
 AUTO_KREG = 96  # write-free scratch tails
 AUTO_KREG_API = 48  # tails of API outputs
 AUTO_KREG_API_PF = 6
+# register band fronts prefetched across section and writer/reader boundaries, AUTO_BAND_PF levels
+# ahead (ring depth + 2): vadv 1024^2x160 1.763 ms against 1.800-1.810 (pf 10 per section) and
+# 1.791 (pf 12 per section, the round-4 default, which spilled 9 registers); span pf 8 1.780,
+# pf 12 1.791; tridiag -0.3 % (profiles/r04/r04n_sweep_*_span_*.log)
+DEFAULT_BAND_SPAN = 1
+BAND_PF_OVER_RING = 2
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -461,8 +467,25 @@ class ColumnGen:
                 ct = self.st.decl(n).dtype.ctype
                 B.append(f"{ct}* __restrict__ {t.var(n)} = ({ct}*)(gtmi_lds + {off});")
                 off = f"{off} + (size_t)p.tail_len * 256 * sizeof({ct})"
+        # prefetch across the writer/reader boundary of the register band (kreg_pf_span): the
+        # reader is rendered first so that the writer's last band levels can issue the reader's
+        # first band prefetches (declared here, at kernel scope)
+        t_ = self.tail
+        self._xpf = bool(self.kreg) and int(self.opts.get("kreg_pf_span", DEFAULT_BAND_SPAN)) == 1 and t_ is not None \
+            and t_.a != t_.b and t_.b in self.kernel.loops and t_.a in self.kernel.loops \
+            and self.kernel.loops.index(t_.b) == self.kernel.loops.index(t_.a) + 1
+        if self._xpf:
+            # a reader front the writer's band might still write (any reader window field the
+            # writer writes, except the band-served tail fields) must not be fetched early
+            wa = self.info[t_.a]
+            clash = {n for (n, _, _) in self.info[t_.b].win} & (wa.wnames | wa.direct)
+            self._xpf = not (clash - set(t_.fields))
+        self._xpf_decls, self._xpf_loads = [], []
+        order = [t_.b] + [x for x in self.kernel.loops if x != t_.b] if self._xpf else list(self.kernel.loops)
+        rendered = {li: self._render_loop(li) for li in order}
+        B += self._xpf_decls
         for li in self.kernel.loops:
-            B += self._render_loop(li)
+            B += rendered[li]
         L += ["    " + x for x in B]
         L.append("}")
         H = [f"{{  // kernel {k}: column, loops {self.kernel.loops}"]
@@ -624,6 +647,56 @@ class ColumnGen:
 
         sec_start = len(out)
         band_code: List[str] = []
+        # register band fronts prefetched across the whole band (option ``kreg_pf_span``): one
+        # sweep-order list of band levels over all sections, each level prefetching the one ``Pb``
+        # levels on whatever section it lies in, and -- for the writer, whose band ends the sweep
+        # -- the prologue issued at the start of the loop, so no band level (nor the first) waits
+        # for loads issued at a section boundary
+        span = bool(R) and int(self.opts.get("kreg_pf_span", DEFAULT_BAND_SPAN)) == 1
+        if R:
+            Pb = int(self.opts.get("kreg_pf", self.band_pf_default if self.band_pf_default is not None else P + BAND_PF_OVER_RING))
+            kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
+            all_us = sorted((u for u in range(R) if band_map[u] is not None), reverse=not fwd)
+            mem_keys = {}
+            for u in all_us:
+                mk = []
+                for key in win:
+                    if not front_load[key] or not self._mem(key[0]):
+                        continue
+                    if key[0] in tail_read and key[1:] == (0, 0) and 0 <= u + front[key] < R:
+                        continue  # served by the register band
+                    mk.append(key)
+                mem_keys[u] = mk
+            pfv = {}
+
+            def prefetch(u_):
+                return [f"{pfv[(u_, key)]} = {mem_index(key[0], key[1], key[2], f'({kexpr_of(u_)}) + ({front[key]})')};"
+                        for key in mem_keys[u_]]
+
+            def declare_pf(us_, indent):
+                d = []
+                for u in us_:
+                    for key in mem_keys[u]:
+                        pfv[(u, key)] = f"bp{u}_{wvar(*key, front[key])}"
+                        d.append(f"{indent}{decl_dtype[key[0]].ctype} {pfv[(u, key)]};")
+                return d
+
+            if span and Pb > 0 and self._xpf and li == tail.b:
+                # reader: its first Pb band levels are prefetched by the writer's last band levels
+                self._xpf_decls = declare_pf(all_us[:Pb], "")
+                self._xpf_loads = [prefetch(u) for u in all_us[:Pb]]
+                out += declare_pf(all_us[Pb:], "    ")
+                sec_start = len(out)
+            elif span and Pb > 0:
+                out += declare_pf(all_us, "    ")
+                out.append("    if (regband) {  // band prefetch prologue (whole band)")
+                for u in all_us[:Pb]:
+                    out += ["        " + x for x in prefetch(u)]
+                if self._xpf and li == tail.a:  # reader levels the writer's band is too short to reach
+                    for j in range(max(0, Pb - len(all_us))):
+                        out += ["        " + x for x in self._xpf_loads[j]]
+                out.append("    }")
+                sec_start = len(out)
         for si, sec in enumerate(vl.sections):
             lo, hi = interval_bounds(sec.interval)
             out.append(f"    {{  // section {si}")
@@ -680,13 +753,16 @@ class ColumnGen:
                             body += load_into(fv, name, di, dj, f"k + ({fd})", maybe_cached=(mode == "mixed"))
                 return body
 
-            def reload(reg_u: Optional[int] = None) -> List[str]:
+            def reload(reg_u: Optional[int] = None, pf: Optional[Dict] = None) -> List[str]:
                 body = []
                 for (name, di, dj), rng in win.items():
                     if not self._mem(name):
                         continue
                     for d in range(rng[0], rng[1] + 1):
                         if d == 0 and not zero_needed_in(name, di, dj, sec):
+                            continue
+                        if pf is not None and (name, di, dj) in pf and d == front[(name, di, dj)]:
+                            body.append(f"{wvar(name, di, dj, d)} = {pf[(name, di, dj)]};")  # prefetched
                             continue
                         body += load_into(wvar(name, di, dj, d), name, di, dj, f"k + ({d})",
                                           reg=None if reg_u is None else reg_u + d)
@@ -855,49 +931,31 @@ class ColumnGen:
                 # band level n's fronts are loaded ``kreg_pf`` band levels earlier into registers
                 # of their own (a level waiting for its own loads stalls a one-wave-per-SIMD kernel)
                 order_us = sorted(us, reverse=not fwd)
-                kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
-                # default: 4 levels deeper than the load ring (vadv 1024^2x160, kreg 96: pf 8 1.854,
-                # 12 1.822, 16 1.914, 24 2.159 ms; profiles/r04/sweep_vadv_band_pf.log)
-                Pb = int(self.opts.get("kreg_pf", self.band_pf_default if self.band_pf_default is not None else P + 4))
-                mem_keys = {}
-                for u in order_us:
-                    mk = []
-                    for key in win:
-                        if not front_load[key] or not self._mem(key[0]):
-                            continue
-                        fd = front[key]
-                        if key[0] in tail_read and key[1:] == (0, 0) and 0 <= u + fd < R:
-                            continue  # served by the register band
-                        mk.append(key)
-                    mem_keys[u] = mk
+                # prefetch distance: see BAND_PF_OVER_RING (per-section prologues, before the span:
+                # pf 8 1.854, 12 1.822, 16 1.914, 24 2.159 ms; profiles/r04/sweep_vadv_band_pf.log)
                 bc = [f"    if (regband) {{  // section {si}: register band levels"]
-                pfv = {}
-                if Pb > 0:
-                    for u in order_us:
-                        for key in mem_keys[u]:
-                            t_ = decl_dtype[key[0]].ctype
-                            pfv[(u, key)] = f"bp{u}_{wvar(*key, front[key])}"
-                            bc.append(f"        {t_} {pfv[(u, key)]};")
-
-                def prefetch(u_):
-                    return [f"{pfv[(u_, key)]} = {mem_index(key[0], key[1], key[2], f'({kexpr_of(u_)}) + ({front[key]})')};"
-                            for key in mem_keys[u_]]
-
-                if Pb > 0:
+                if Pb > 0 and not span:
+                    bc += declare_pf(order_us, "        ")
                     bc.append("        // band prefetch prologue")
                     for u in order_us[:Pb]:
                         bc += ["        " + x for x in prefetch(u)]
+                seq = all_us if span else order_us
                 for n_, u in enumerate(order_us):
                     kexpr = kexpr_of(u)
                     reg_now[0], band_now[0] = u, "reg"
                     pf = {key: pfv[(u, key)] for key in mem_keys[u]} if Pb > 0 else None
                     if n_ == 0:
-                        body = (["if (k != k_next) {"] + ["    " + x for x in reload(u)] + ["} else {"]
+                        body = (["if (k != k_next) {"] + ["    " + x for x in reload(u, pf if span else None)] + ["} else {"]
                                 + ["    " + x for x in shift_and_fronts(None, "mem", u, pf)] + ["}"])
                     else:
                         body = shift_and_fronts(None, "mem", u, pf)
-                    if Pb > 0 and n_ + Pb < len(order_us):
-                        body += prefetch(order_us[n_ + Pb])
+                    g_ = seq.index(u)
+                    if Pb > 0 and g_ + Pb < len(seq):
+                        body += prefetch(seq[g_ + Pb])
+                    elif span and self._xpf and li == tail.a and Pb > 0:
+                        j_ = g_ + Pb - len(seq)
+                        if 0 <= j_ < len(self._xpf_loads):
+                            body += ["// the reader's band: prefetched here"] + self._xpf_loads[j_]
                     body += statements()
                     reg_now[0], band_now[0] = None, None
                     bc.append(f"        {{  const int k = {kexpr};")
