@@ -47,6 +47,14 @@ AUTO_KREG_API_PF = 6
 # pf 12 1.791; tridiag -0.3 % (profiles/r04/r04n_sweep_*_span_*.log)
 DEFAULT_BAND_SPAN = 1
 BAND_PF_OVER_RING = 2
+# light streams (at most LIGHT_OPS memory operations per level, loads + stores) move too few bytes
+# per level for a 10-level prefetch to cover HBM latency with one wave per SIMD (vadv's backward
+# sweep: one load, one store): option ``kpf_adapt`` deepens their band prefetch and load ring to
+# VM_SLOTS // ops levels (at most ADAPT_MAX); loads and stores share the 6-bit vmcnt
+DEFAULT_PF_ADAPT = 0
+LIGHT_OPS = 3
+VM_SLOTS = 48
+ADAPT_MAX = 32
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -653,6 +661,8 @@ class ColumnGen:
         # -- the prologue issued at the start of the loop, so no band level (nor the first) waits
         # for loads issued at a section boundary
         span = bool(R) and int(self.opts.get("kreg_pf_span", DEFAULT_BAND_SPAN)) == 1
+        # memory fields this loop stores at every level (the band's no-store scratch aside)
+        loop_stores = {n for n in wnames if self._mem(n) and n not in direct and n not in no_store}
         if R:
             Pb = int(self.opts.get("kreg_pf", self.band_pf_default if self.band_pf_default is not None else P + BAND_PF_OVER_RING))
             kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
@@ -668,6 +678,10 @@ class ColumnGen:
                     mk.append(key)
                 mem_keys[u] = mk
             pfv = {}
+            if int(self.opts.get("kpf_adapt", DEFAULT_PF_ADAPT)) == 1 and "kreg_pf" not in self.opts and all_us:
+                n_ops = max(len(mem_keys[u]) for u in all_us) + len(loop_stores)
+                if 0 < n_ops <= LIGHT_OPS:
+                    Pb = max(Pb, min(ADAPT_MAX, VM_SLOTS // n_ops))
 
             def prefetch(u_):
                 return [f"{pfv[(u_, key)]} = {mem_index(key[0], key[1], key[2], f'({kexpr_of(u_)}) + ({front[key]})')};"
@@ -681,19 +695,33 @@ class ColumnGen:
                         d.append(f"{indent}{decl_dtype[key[0]].ctype} {pfv[(u, key)]};")
                 return d
 
+            # span schedule: ``pre`` levels are in flight when the band starts (the prologue, or for
+            # the reader the writer's last levels: at most the default distance, which the writer's
+            # registers afford); the rest are issued at most two per level, each ``Pb`` levels
+            # ahead or as early as that allows, so a deeper distance ramps up within the band
+            issue_at: Dict[int, List[int]] = {}
+            if span and Pb > 0:
+                pre = Pb
+                if self._xpf and li == tail.b:
+                    pre = min(Pb, int(self.opts.get("kreg_pf", P + BAND_PF_OVER_RING)))
+                pre = min(pre, len(all_us))
+                pend = list(range(pre, len(all_us)))
+                for p_ in range(len(all_us)):
+                    while pend and pend[0] - Pb <= p_ and len(issue_at.get(p_, ())) < 2:
+                        issue_at.setdefault(p_, []).append(pend.pop(0))
             if span and Pb > 0 and self._xpf and li == tail.b:
-                # reader: its first Pb band levels are prefetched by the writer's last band levels
-                self._xpf_decls = declare_pf(all_us[:Pb], "")
-                self._xpf_loads = [prefetch(u) for u in all_us[:Pb]]
-                out += declare_pf(all_us[Pb:], "    ")
+                # reader: its first ``pre`` band levels are prefetched by the writer's last band levels
+                self._xpf_decls = declare_pf(all_us[:pre], "")
+                self._xpf_loads = [prefetch(u) for u in all_us[:pre]]
+                out += declare_pf(all_us[pre:], "    ")
                 sec_start = len(out)
             elif span and Pb > 0:
                 out += declare_pf(all_us, "    ")
                 out.append("    if (regband) {  // band prefetch prologue (whole band)")
-                for u in all_us[:Pb]:
+                for u in all_us[:pre]:
                     out += ["        " + x for x in prefetch(u)]
                 if self._xpf and li == tail.a:  # reader levels the writer's band is too short to reach
-                    for j in range(max(0, Pb - len(all_us))):
+                    for j in range(max(0, len(self._xpf_loads) - len(all_us))):
                         out += ["        " + x for x in self._xpf_loads[j]]
                 out.append("    }")
                 sec_start = len(out)
@@ -825,7 +853,12 @@ class ColumnGen:
                 """Levels [ss, se) of the section in sweep order. ``mode``: "mem" (no front of
                 these levels is tail-cached), "lds" (every tail-cached front is), "mixed"."""
                 keys = [k_ for k_ in ring_keys if not (mode == "lds" and k_ in tail_keys)] if mode != "mixed" else []
-                R = _section_ring(sec.interval, P) if keys else 0
+                Pseg = P
+                if keys and int(self.opts.get("kpf_adapt", DEFAULT_PF_ADAPT)) == 1 and "kring" not in self.opts:
+                    n_ops = len(keys) + len(loop_stores)
+                    if n_ops <= LIGHT_OPS:
+                        Pseg = max(P, min(ADAPT_MAX, VM_SLOTS // n_ops))
+                R = _section_ring(sec.interval, Pseg) if keys else 0
                 o = [f"{{  // levels [{ss}, {se}), {mode}"]
                 o.append(f"    const int ss = {ss}, se = {se};")
                 first = "ss" if fwd else "se - 1"
@@ -950,10 +983,15 @@ class ColumnGen:
                     else:
                         body = shift_and_fronts(None, "mem", u, pf)
                     g_ = seq.index(u)
-                    if Pb > 0 and g_ + Pb < len(seq):
+                    if span:
+                        for t_ in issue_at.get(g_, ()):
+                            body += prefetch(seq[t_])
+                    elif Pb > 0 and g_ + Pb < len(seq):
                         body += prefetch(seq[g_ + Pb])
-                    elif span and self._xpf and li == tail.a and Pb > 0:
-                        j_ = g_ + Pb - len(seq)
+                    if span and self._xpf and li == tail.a and Pb > 0:
+                        # the reader's band level j is prefetched its own distance (len(_xpf_loads))
+                        # before the reader starts
+                        j_ = g_ + len(self._xpf_loads) - len(seq)
                         if 0 <= j_ < len(self._xpf_loads):
                             body += ["// the reader's band: prefetched here"] + self._xpf_loads[j_]
                     body += statements()
