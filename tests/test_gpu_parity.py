@@ -105,7 +105,7 @@ COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tai
                     "vertical_advection_dycore_k160"]
 COLUMN_OPTS = [{"kreg": 32}, {"kreg": 16, "seg_tail": 1}, {"seg_tail": 1}, {"ktail_lds": 0}, {"kring": 3},
                {"kreg": 96}, {"kreg": 64, "kreg_pf": 0}, {"kreg": 48, "kreg_pf": 3}, {"kreg_pf_span": 0},
-               {"kreg": 40, "kreg_pf": 50}]
+               {"kreg": 40, "kreg_pf": 50}, {"kpf_adapt": 1}]
 
 
 @pytest.mark.parametrize("opts", COLUMN_OPTS, ids=lambda o: "_".join(f"{k}{v}" for k, v in o.items()))
