@@ -52,6 +52,10 @@ BAND_PF_OVER_RING = 2
 # sweep: one load, one store): option ``kpf_adapt`` deepens their band prefetch and load ring to
 # VM_SLOTS // ops levels (at most ADAPT_MAX); loads and stores share the 6-bit vmcnt
 DEFAULT_PF_ADAPT = 0
+# I-neighbour reads from lane shifts (option ``nbr_shfl``): a field read at (+-1, 0) next to its
+# own column takes the neighbour lane's load (DPP wave rotate) plus one wave-uniform load of the
+# column past the wave, instead of a second, misaligned 64-lane load per level
+DEFAULT_NBR = 0
 LIGHT_OPS = 3
 VM_SLOTS = 48
 ADAPT_MAX = 32
@@ -112,6 +116,10 @@ class ColumnGen:
             if ti and not 8 <= ti <= bx - ilo - ihi:
                 raise ValueError(f"tile_ti must be in [8, {bx - ilo - ihi}] for IJ extent {self.ext}, got {ti}")
         self.info = {li: self._analyse_loop(li) for li in kernel.loops}
+        self.nbr = {li: self._nbr_plan(li) for li in kernel.loops}
+        if not any(self.nbr.values()) or self._has_while():
+            self.nbr = {li: {} for li in kernel.loops}
+        self.nbr_on = any(self.nbr.values())
         self.kreg = 0
         self.band_pf_default = None
         self.tail = None if self.tile else self._plan_tail()
@@ -237,6 +245,39 @@ class ColumnGen:
                 # cannot carry a value across levels that never run
                 raise UnsupportedStencil(f"register temporary '{name}' read at a K offset across a section gap")
         return _LoopInfo(vl.loop_order != ir.LoopOrder.BACKWARD, direct, win, wnames)
+
+    def _nbr_plan(self, li) -> Dict[Tuple[str, int, int], Tuple[Tuple[str, int, int], int]]:
+        """Window keys ``(name, +-1, 0)`` that the I-neighbour lane shift can serve: a memory field
+        this loop does not write, also read at ``(0, 0)`` with the same window front and a window
+        that covers the neighbour's (so every neighbour entry has its own-column twin)."""
+        out = {}
+        if self.tile or int(self.opts.get("nbr_shfl", DEFAULT_NBR)) != 1:
+            return out
+        inf = self.info[li]
+        for (name, di, dj), rng in inf.win.items():
+            if dj != 0 or di not in (1, -1) or not self._mem(name) or name in inf.wnames or name in inf.direct:
+                continue
+            base = inf.win.get((name, 0, 0))
+            if base is None or rng[0] < base[0] or rng[1] > base[1]:
+                continue
+            if (rng[1] if inf.fwd else rng[0]) != (base[1] if inf.fwd else base[0]):
+                continue
+            out[(name, di, dj)] = ((name, 0, 0), di)
+        return out
+
+    def _has_while(self) -> bool:
+        """A data-dependent loop in the kernel: lanes past the domain (kept alive for the shuffles)
+        would run it on garbage."""
+        def walk(stmts):
+            for x in stmts:
+                if isinstance(x, ir.While):
+                    return True
+                if isinstance(x, ir.If) and (walk(x.body) or walk(x.orelse or [])):
+                    return True
+                if isinstance(x, ir.HorizontalRegion) and walk(x.body):
+                    return True
+            return False
+        return any(walk(sec.body) for li in self.kernel.loops for sec in self.st.vertical_loops[li].sections)
 
     def _plan_tail(self) -> Optional[_Tail]:
         budget = int(self.opts.get("ktail_lds", LDS_BYTES))
@@ -434,7 +475,15 @@ class ColumnGen:
             B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x) - {eilo};")
             B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y) - {ejlo};")
         if not self.tile:
-            B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
+            if self.nbr_on:
+                # whole waves only (j is wave-uniform): the I-neighbour shuffles need every lane, so
+                # lanes past the domain in I stay, compute on clamped loads and store nothing
+                B.append(f"if (j >= p.nj + {ejhi}) return;")
+                B.append(f"const bool ialive = i < p.ni + {eihi};")
+                B.append("const int gi0_ = __builtin_amdgcn_readfirstlane(i - (int)(threadIdx.x & 63));")
+                B.append("const int gj_ = __builtin_amdgcn_readfirstlane(j);")
+            else:
+                B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
         B.append("const int nk = p.nk;")
         for s in scalars:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
@@ -452,6 +501,19 @@ class ColumnGen:
                 for acc, w in iter_accesses(sec.body):
                     if isinstance(acc, ir.FieldAccess) and acc.name in inf.direct:
                         self._base(acc.name, acc.offset[0], acc.offset[1], B, acc.name in written)
+        # I-neighbour edges: the one column past the wave (D = 1) or before it (D = -1), wave-uniform
+        self.edge_bases: Dict[Tuple[str, int], str] = {}
+        for li in self.kernel.loops:
+            for (name, di, _dj) in self.nbr[li]:
+                if (name, di) in self.edge_bases:
+                    continue
+                c = cname(name)
+                v = f"ce_{c}_{_sgn(di)}"
+                t = self.st.decl(name).dtype.ctype
+                col = "gi0_ + 64" if di == 1 else "gi0_ - 1"
+                B.append(f"const {t}* __restrict__ {v} = p.p_{c} + ((int64_t)gtmi::clampi({col}, p.ilo_{c}, p.ihi_{c}) * "
+                         f"p.sI_{c} + (int64_t)gtmi::clampi(gj_, p.jlo_{c}, p.jhi_{c}) * p.sJ_{c});")
+                self.edge_bases[(name, di)] = v
         if self.tail is not None:
             t = self.tail
             B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
@@ -572,10 +634,23 @@ class ColumnGen:
             c = cname(name)
             return f"({self.bases[(name, di, dj)]} + (int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
 
+        derived = self.nbr.get(li, {})
+
         def mem_index(name, di, dj, kexpr):
-            """A load expression (non-temporal for read-once streams)."""
+            """A load expression (non-temporal for read-once streams). For an I-neighbour key the
+            lane shift serves (``derived``) it is the wave-uniform edge load only; see ``nbr_of``."""
+            if (name, di, dj) in derived:
+                c = cname(name)
+                ptr = f"({self.edge_bases[(name, di)]} + (int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
+                return f"gtmi::uload<{decl_dtype[name].ctype}>({ptr})"
             nt = "true" if (name in self.nt_loads and name not in direct) else "false"
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
+
+        def nbr_of(key, d, edge):
+            """Window entry ``d`` of I-neighbour key ``key``: the own-column entry of the neighbour
+            lane, the wave's edge column from ``edge``."""
+            (bname, bdi, bdj), D = derived[key]
+            return f"gtmi::nbr<{D}>({wvar(bname, bdi, bdj, d)}, {edge})"
 
         def load_into(var, name, di, dj, kexpr, maybe_cached=True, reg=None) -> List[str]:
             """``var = F(level kexpr)``: from the LDS tail cache when this loop reads a cached level
@@ -604,6 +679,8 @@ class ColumnGen:
                     return "// cached level: kept in LDS only"
                 if band_now[0] is None:
                     st = f"if (k < tc0 || k >= tc1) {st}"
+            if self.nbr_on:
+                st = f"if (ialive) {st}"
             return st
 
         P = self.ring
@@ -757,7 +834,7 @@ class ColumnGen:
                 index), from a band prefetch register (``pf``: key -> variable) or from memory here
                 (``slot`` None)."""
                 body = []
-                for key, rng in win.items():
+                for key, rng in sorted(win.items(), key=lambda kv: kv[0] in derived):
                     name, di, dj = key
                     ds = list(range(rng[0], rng[1] + 1))
                     if fwd:
@@ -766,7 +843,17 @@ class ColumnGen:
                     else:
                         for d in reversed(ds[1:]):
                             body.append(f"{wvar(name, di, dj, d)} = {wvar(name, di, dj, d - 1)};")
-                    if front_load[key]:
+                    if front_load[key] and key in derived:
+                        fd = front[key]
+                        fv = wvar(name, di, dj, fd)
+                        if pf is not None and key in pf:
+                            edge = pf[key]
+                        elif slot is not None and key in ring_keys and reg_u is None:
+                            edge = f"rg{slot}_{fv}"
+                        else:
+                            edge = mem_index(name, di, dj, f"k + ({fd})")
+                        body.append(f"{fv} = {nbr_of(key, fd, edge)};")
+                    elif front_load[key]:
                         fd = front[key]
                         fv = wvar(name, di, dj, fd)
                         if pf is not None and key in pf:
@@ -783,11 +870,17 @@ class ColumnGen:
 
             def reload(reg_u: Optional[int] = None, pf: Optional[Dict] = None) -> List[str]:
                 body = []
-                for (name, di, dj), rng in win.items():
+                for (name, di, dj), rng in sorted(win.items(), key=lambda kv: kv[0] in derived):
                     if not self._mem(name):
                         continue
                     for d in range(rng[0], rng[1] + 1):
                         if d == 0 and not zero_needed_in(name, di, dj, sec):
+                            continue
+                        if (name, di, dj) in derived:
+                            key_ = (name, di, dj)
+                            edge = pf[key_] if (pf is not None and key_ in pf and d == front[key_]) else \
+                                mem_index(name, di, dj, f"k + ({d})")
+                            body.append(f"{wvar(name, di, dj, d)} = {nbr_of(key_, d, edge)};")
                             continue
                         if pf is not None and (name, di, dj) in pf and d == front[(name, di, dj)]:
                             body.append(f"{wvar(name, di, dj, d)} = {pf[(name, di, dj)]};")  # prefetched
