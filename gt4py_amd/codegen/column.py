@@ -251,7 +251,7 @@ class ColumnGen:
         this loop does not write, also read at ``(0, 0)`` with the same window front and a window
         that covers the neighbour's (so every neighbour entry has its own-column twin)."""
         out = {}
-        if self.tile or int(self.opts.get("nbr_shfl", DEFAULT_NBR)) != 1:
+        if self.tile or int(self.opts.get("nbr_shfl", DEFAULT_NBR)) not in (1, 2):
             return out
         inf = self.info[li]
         for (name, di, dj), rng in inf.win.items():
@@ -642,6 +642,8 @@ class ColumnGen:
             if (name, di, dj) in derived:
                 c = cname(name)
                 ptr = f"({self.edge_bases[(name, di)]} + (int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
+                if int(self.opts.get("nbr_shfl", DEFAULT_NBR)) == 2:  # vector load, uniform address
+                    return f"gtmi::sload<{decl_dtype[name].ctype}, false>({ptr})"
                 return f"gtmi::uload<{decl_dtype[name].ctype}>({ptr})"
             nt = "true" if (name in self.nt_loads and name not in direct) else "false"
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"

@@ -3,9 +3,9 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r04s
+O=gpurun_out/r04t
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "neighbour or column_options or vadv" --timeout 120 --timeout-method thread > $O/pytest_nbr.log 2>&1 \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "neighbour" --timeout 120 --timeout-method thread > $O/pytest_nbr.log 2>&1 \
   || { tail -40 $O/pytest_nbr.log; exit 1; }
 tail -2 $O/pytest_nbr.log
 for rep in 1 2; do

@@ -307,7 +307,8 @@ def nbr_column(a: F64, b: F64, c: F64, out: F64):
             out = out[0, 0, -1] * 0.5 + (a[1, 0, 0] - a[-1, 0, 0]) + b[1, 0, -1] * b[0, 0, 0] - a[0, 0, 0] * c[-1, 0, 0]
 
 
-@pytest.mark.parametrize("opts", [{"nbr_shfl": 1}, {"nbr_shfl": 1, "col_bx": 128}, {"nbr_shfl": 1, "kring": 3}])
+@pytest.mark.parametrize("opts", [{"nbr_shfl": 1}, {"nbr_shfl": 1, "col_bx": 128}, {"nbr_shfl": 1, "kring": 3},
+                                  {"nbr_shfl": 2}])
 def test_neighbour_lane_shift_vs_numpy_backend(opts):
     """I-neighbour reads served by DPP lane shifts plus one wave-uniform edge load (``nbr_shfl``):
     ragged I extents (lanes past the domain stay alive for the shuffles and store nothing),
