@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Drop in-tree cache entries (.gt_cache/gt_mi355x/<key>) that no current build uses.
 
-    python scripts/prune_cache.py            # runs __graft_entry__.build() + the sweep prebuilds
-                                             # with GTMI_CACHE_LOG set, then deletes the rest
+    python scripts/prune_cache.py            # runs __graft_entry__.build() (which prebuilds the GPU
+                                             # tests' libraries too) + the sweep prebuilds with
+                                             # GTMI_CACHE_LOG set, then deletes the rest
     python scripts/prune_cache.py --dry-run
 
 Every call of gpurun sends the whole tree; libraries of superseded code generations only add to

@@ -12,3 +12,12 @@ for p in (REPO, os.path.join(REPO, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+if os.environ.get("GTMI_PREBUILD_TESTS"):
+    # build-container prebuild of the GPU tests' libraries (__graft_entry__.build): every GPU test
+    # runs up to its first device allocation, so the gt:mi355x stencils it constructs before that
+    # are compiled into the in-tree cache the GPU box then loads; the tests themselves fail here
+    import torch
+
+    torch.cuda.is_available = lambda: True
