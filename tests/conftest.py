@@ -20,4 +20,14 @@ if os.environ.get("GTMI_PREBUILD_TESTS"):
     # are compiled into the in-tree cache the GPU box then loads; the tests themselves fail here
     import torch
 
+    import gt4py_amd.storage as _gt_storage
+
+    from gt4py_amd.runtime import launcher as _gt_launcher
+
     torch.cuda.is_available = lambda: True
+    _gt_storage._device_of = lambda info: "cpu"  # tests that allocate first reach their stencils
+
+    def _no_launch(self, *args, **kwargs):
+        raise RuntimeError("GTMI_PREBUILD_TESTS: built, not launched")
+
+    _gt_launcher.StencilLauncher.__call__ = _no_launch
