@@ -253,17 +253,17 @@ def test_data_dimensions(backend):
             field_out[0, 0, 0][0] = 0.0
             field_out[0, 0, 0][1] = 1.0
 
+    @gtscript.stencil(backend=backend)
+    def one(field_out: gtscript.Field[gtscript.IJ, (np.float64, (1,))]):
+        with computation(FORWARD), interval(...):
+            field_out[0, 0][0] = 42.0
+
     with pytest.raises(ValueError, match="Field '.*' expects data dimensions \\(2,\\) but got \\(3,\\)"):
         st(field_out=gt_storage.empty((3, 3, 1), (np.float64, (3,)), backend=backend, aligned_index=(0, 0, 0)))
     f = gt_storage.full((3, 3, 1), 5.0, (np.float64, (2,)), backend=backend, aligned_index=(0, 0, 0))
     st(field_out=f)
     h = _host(f)
     assert (h[..., 0] == 0).all() and (h[..., 1] == 1).all()
-
-    @gtscript.stencil(backend=backend)
-    def one(field_out: gtscript.Field[gtscript.IJ, (np.float64, (1,))]):
-        with computation(FORWARD), interval(...):
-            field_out[0, 0][0] = 42.0
 
     ones = gt_storage.ones((2, 3), (np.float64, (1,)), backend=backend, aligned_index=(0, 0), dimensions=["I", "J"])
     one(ones)

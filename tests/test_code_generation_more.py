@@ -137,15 +137,15 @@ def test_2d_temporaries(backend):
         with computation(FORWARD), interval(...):
             out_field = tmp_2D
 
-    test_with_plain_gt4py(in_arr, out_arr)
-    assert (cpu(out_arr) == domain[2]).all()
-
     @gtscript.stencil(backend=backend, dtypes={"MyFancySymbol": Field[IJ, np.float64]})
     def test_with_user_dtype(in_field: Field[np.float64], out_field: Field[np.float64]) -> None:
         with computation(FORWARD), interval(0, 1):
             tmp_2D: MyFancySymbol = 0  # noqa: F821
         with computation(FORWARD), interval(...):
             out_field = tmp_2D
+
+    test_with_plain_gt4py(in_arr, out_arr)
+    assert (cpu(out_arr) == domain[2]).all()
 
     out_arr = storage.full(domain, 9.0, np.float64, backend=backend)
     test_with_user_dtype(in_arr, out_arr)
