@@ -429,7 +429,33 @@ class ColumnGen:
                 if self._mem(n) and n not in self.scratch and not (read_loops.get(n, set()) - wl)
             }
         scalars = st.scalar_params()
-        L = [f"struct K{k}Params {{"]
+        L = []
+        if self.nbr_on:
+            # I-neighbour helpers, emitted only by kernels that use them (the device header, which
+            # every library key hashes, stays as it is)
+            L += [
+                "#ifndef GTMI_NBR_HELPERS",
+                "#define GTMI_NBR_HELPERS",
+                "namespace gtmi {",
+                "// a field's value one column over (I + D) from the wave's own loads: lane l takes lane",
+                "// l + D's value; the lane whose neighbour lies in the next (D = 1) or previous (D = -1) wave",
+                "// takes ``edge``, one wave-uniform load of that column. Every lane of the wave must be live.",
+                "template <int D, typename T> GTMI_DEV T nbr(T base, T edge) {",
+                "    const T s = shfl_c<D>(base);",
+                "    const int lane = (int)__lane_id();",
+                "    return (D == 1 ? lane == 63 : lane == 0) ? edge : s;",
+                "}",
+                "// a wave-uniform load of memory the kernel only reads, through the constant address space",
+                "template <typename T> GTMI_DEV T uload(const T* p) {",
+                "    using G = const __attribute__((address_space(1))) T;",
+                "    using C = const __attribute__((address_space(4))) T;",
+                "    return *(C*)(G*)p;",
+                "}",
+                "}  // namespace gtmi",
+                "#endif",
+                "",
+            ]
+        L.append(f"struct K{k}Params {{")
         for s in used:
             L += ["    " + x for x in kparam_decl(s, s.name in written)]
         for s in scalars:

@@ -74,16 +74,6 @@ template <int D, typename T> GTMI_DEV T shfl_c(T v) {
     }
 }
 
-// Column kernels: a field's value one column over (I + D) from the wave's own loads: lane l takes
-// lane l + D's value; the lane whose neighbour lies in the next (D = 1) or the previous (D = -1)
-// wave takes ``edge``, one wave-uniform load of that column. Every lane of the wave must be live.
-template <int D, typename T> GTMI_DEV T nbr(T base, T edge) {
-    static_assert(D == 1 || D == -1, "one column over only");
-    const T s = shfl_c<D>(base);
-    const int lane = (int)__lane_id();
-    return (D == 1 ? lane == 63 : lane == 0) ? edge : s;
-}
-
 // ---------------------------------------------------------------- clamps
 GTMI_DEV int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
@@ -243,13 +233,6 @@ template <typename T, int V, bool NT> GTMI_DEV void bstore(__amdgpu_buffer_rsrc_
 }
 template <typename T, bool NT> GTMI_DEV T sload(const T* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p); else return *p;
-}
-// A wave-uniform load of memory the kernel only reads (column kernels' I-neighbour edges): through
-// the constant address space, so the compiler can use the scalar cache for it.
-template <typename T> GTMI_DEV T uload(const T* p) {
-    using G = const __attribute__((address_space(1))) T;
-    using C = const __attribute__((address_space(4))) T;
-    return *(C*)(G*)p;
 }
 template <typename T, bool NT> GTMI_DEV void sstore(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
