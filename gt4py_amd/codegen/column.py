@@ -778,6 +778,8 @@ class ColumnGen:
                 for key in win:
                     if not front_load[key] or not self._mem(key[0]):
                         continue
+                    if key[0] in wnames and "K" not in self.st.decl(key[0]).axes:
+                        continue  # as ring_keys: one address for every level, loaded at its level
                     if key[0] in tail_read and key[1:] == (0, 0) and 0 <= u + front[key] < R:
                         continue  # served by the register band
                     mk.append(key)

@@ -2179,6 +2179,52 @@ case("tail_bwd_fwd", fields={"a": fs(6, 5, 130), "c": fs(6, 5, 130), "out": fs(6
 case("tail_bwd_fwd_short", fields={"a": fs(6, 5, 9), "c": fs(6, 5, 9), "out": fs(6, 5, 9, init="zeros")})(tail_bwd_fwd)
 
 
+def band_ij_accumulator(a: F64, b: F64, out: F64, s: F2D, lev: Field[IJ, np.int32]):
+    """A FORWARD sweep producing a tail-cached temporary ``c`` next to an IJ counter ``lev``, then
+    a BACKWARD sweep accumulating into the IJ field ``s`` at every level. With nk above the
+    register band's minimum (96 levels) both IJ accumulators are read and written inside the band:
+    a front of them loaded levels ahead would miss the writes in between."""
+    with computation(FORWARD):
+        with interval(0, 1):
+            c = a
+            lev = 0
+        with interval(1, None):
+            c = a + 0.5 * c[0, 0, -1]
+            lev = lev + 1
+    with computation(BACKWARD):
+        with interval(-1, None):
+            s = c * b
+            out = s
+        with interval(0, -1):
+            s = s * 0.5 + c * b
+            out = s + lev
+
+
+def band_ij_accumulator_reader(a: F64, b: F64, out: F64, s: F2D):
+    """As ``band_ij_accumulator`` with the IJ accumulator in the reader only, so the writer's last
+    band levels prefetch the reader's first ones (kreg_pf_span across the loop boundary)."""
+    with computation(FORWARD):
+        with interval(0, 1):
+            c = a
+        with interval(1, None):
+            c = a + 0.5 * c[0, 0, -1]
+    with computation(BACKWARD):
+        with interval(-1, None):
+            s = c * b
+            out = s
+        with interval(0, -1):
+            s = s * 0.5 + c * b
+            out = s - a
+
+
+case("band_ij_accumulator", fields={"a": fs(9, 4, 120), "b": fs(9, 4, 120), "out": fs(9, 4, 120, init="zeros"),
+                                    "s": fs(9, 4), "lev": fs(9, 4, dtype="i4", init=("int", 50, 60))})(
+    band_ij_accumulator)
+case("band_ij_accumulator_reader", fields={"a": fs(9, 4, 131), "b": fs(9, 4, 131),
+                                           "out": fs(9, 4, 131, init="zeros"), "s": fs(9, 4)})(
+    band_ij_accumulator_reader)
+
+
 # --------------------------------------------------------------------------------------
 # Tile kernels (column kernels in tile mode, codegen/column.py): sequential sweeps that read
 # their own products across columns -- the reference's IJ caches

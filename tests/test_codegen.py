@@ -127,3 +127,18 @@ def test_row_unroll_auto_rule():
         copies = set(int(m) for m in re.findall(r"// row copy (\d+)", src))
         assert copies == (set(range(u)) if u else set()), (name, copies)
         assert ("// slot copy 0" in src) == slots, name
+
+
+@pytest.mark.parametrize("opts", [{}, {"kreg_pf_span": 0}, {"kreg": 40, "kreg_pf": 50}])
+@pytest.mark.parametrize("name", ["band_ij_accumulator", "band_ij_accumulator_reader"])
+def test_register_band_never_prefetches_written_ij_fields(name, opts):
+    """A field a loop both reads and writes that has no K axis (an IJ accumulator) is one address
+    for every level: the register band must load it at its level, never levels ahead (ADVICE r04,
+    high). Fields with a K axis, and IJ fields the loop only reads, may still be prefetched."""
+    case = sc.CASES[name]
+    st = gtscript.stencil(backend="gt:mi355x", definition=case.definition, name=f"gpu.{name}", **opts)
+    src = st._gt_run_impl_.compiled.source
+    assert "regband" in src
+    prefetched = set(re.findall(r"\bbp\d+_w(\d+)_(\w+?)_p0_p0_", src))
+    assert ("1", "s") not in prefetched and ("0", "lev") not in prefetched, prefetched
+    assert {n for _, n in prefetched} >= {"a", "b"}

@@ -105,7 +105,7 @@ def test_golden_case(name):
 COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tail_bwd_fwd", "tail_bwd_fwd_short",
                     "tail_fwd_bwd_offsets", "tridiag", "tridiag_k161", "tridiag_k2", "tridiag_k70",
                     "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80",
-                    "vertical_advection_dycore_k160"]
+                    "vertical_advection_dycore_k160", "band_ij_accumulator", "band_ij_accumulator_reader"]
 COLUMN_OPTS = [{"kreg": 32}, {"kreg": 16, "seg_tail": 1}, {"seg_tail": 1}, {"ktail_lds": 0}, {"kring": 3},
                {"kreg": 96}, {"kreg": 64, "kreg_pf": 0}, {"kreg": 48, "kreg_pf": 3}, {"kreg_pf_span": 0},
                {"kreg": 40, "kreg_pf": 50}, {"kpf_adapt": 1}, {"nbr_shfl": 1}]
