@@ -340,6 +340,23 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
         med2 = median_s(second[1])
         rec["second_input"] = {"inputs": second[0], "value": round(cells / med2 / 1e6, 2), "unit": "Mcells/s",
                                "ms_per_call": round(med2 * 1e3, 3)}
+    if sname == "horizontal_diffusion" and threads > 1:
+        # thread scaling of the same code on a K-slab sample: the pool's rules
+        # cap a one-GPU job at its CPU share, so the all-core figure is not run; the curve up to the
+        # share says how the figure grows with cores
+        ks = min(nk, 16)
+        curve = []
+        for t in sorted({1, 2, 4, 8, threads} & set(range(1, threads + 1))):
+            f = lambda t=t: c_oracle.horizontal_diffusion(a, o, c, org, (ni, nj, ks), nthreads=t)  # noqa: E731
+            for _ in range(1):
+                f()
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                f()
+                ts.append(time.perf_counter() - t0)
+            curve.append({"threads": t, "Mcells_s": round(ni * nj * ks / float(np.median(ts)) / 1e6, 2)})
+        rec["thread_scaling"] = {"sample": f"{ni}x{nj}x{ks} slab of the same inputs, median of 5 calls", "curve": curve}
     return rec
 
 
@@ -745,6 +762,80 @@ def sharded_leg(cfg, args, rank, world, dev, backend, dist) -> dict:
 # ------------------------------------------------------------------------------------------
 
 
+class RankPhase:
+    """Bounded set-up of an N-rank run: a daemon thread ends the rank with
+    exit status 3 and its last phase on stderr if process-group set-up, the first collectives and
+    the link probe have not completed within ``limit_s`` (``GTMI_DIST_SETUP_TIMEOUT``, default
+    300 s) -- a rank stuck in a rendezvous or a first RCCL call then fails the launch with a
+    reason instead of hanging it. Nothing is re-executed."""
+
+    def __init__(self, rank: int, limit_s: float):
+        import threading
+
+        self.rank, self.limit, self.name, self.t0 = rank, limit_s, "start", time.time()
+        self.history = []
+        self._done = threading.Event()
+        threading.Thread(target=self._watch, name="gtmi-rank-phase", daemon=True).start()
+
+    def set(self, name: str) -> None:
+        self.history.append((name, round(time.time() - self.t0, 3)))
+        self.name = name
+
+    def finish(self) -> None:
+        self.set("setup done")
+        self._done.set()
+
+    def _watch(self) -> None:
+        if not self._done.wait(self.limit):
+            sys.stderr.write(f"bench.py rank {self.rank}: no progress past phase '{self.name}' after "
+                             f"{self.limit:.0f} s (phases so far: {self.history}); exiting with status 3\n")
+            sys.stderr.flush()
+            os._exit(3)
+
+
+def probe_peers(rank, world, dec2d, selfcomm=False):
+    """The ranks this rank exchanges halos with: J-strip neighbours, or the (up to eight) 2-D
+    neighbours incl. corners; itself for the one-GPU self-exchange."""
+    if selfcomm and world == 1:
+        return [0]
+    if dec2d is None:
+        return sorted({r for r in (rank - 1, rank + 1) if 0 <= r < world})
+    ci, cj = dec2d.coords(rank)
+    peers = {dec2d.rank_of(ci + di, cj + dj) for di in (-1, 0, 1) for dj in (-1, 0, 1) if (di, dj) != (0, 0)}
+    return sorted(p for p in peers if p is not None and p != rank)
+
+
+def link_probe(dist, dev, rank, peers, nbytes=10_485_760, reps=3) -> dict:
+    """One face-sized message (10.5 MB, the C5 f32 tile's 2-row J face: 8192 x 2 x 160 x 4 B) to
+    and from every peer in one ``batch_isend_irecv``, timed after a warm-up exchange: per-rank
+    milliseconds and GB/s per link and direction, before the headline runs."""
+    import torch
+
+    tdev = dev if str(dist.get_backend()).lower() == "nccl" else torch.device("cpu")
+    n = nbytes // 4
+    send = {p: torch.full((n,), float(rank), dtype=torch.float32, device=tdev) for p in peers}
+    recv = {p: torch.empty(n, dtype=torch.float32, device=tdev) for p in peers}
+
+    def once():
+        ops = [dist.P2POp(dist.isend, send[p], p) for p in peers] + [dist.P2POp(dist.irecv, recv[p], p) for p in peers]
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        if tdev.type == "cuda":
+            torch.cuda.synchronize(tdev)
+
+    once()  # connections and buffers are set up by the first exchange
+    ok = all(float(recv[p][0]) == float(p) and float(recv[p][-1]) == float(p) for p in peers)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    sec = (time.perf_counter() - t0) / reps
+    return {"rank": rank, "peers": peers, "bytes_per_message": n * 4, "ms": round(sec * 1e3, 4),
+            "GBps_per_link_each_way": round(n * 4 / sec / 1e9, 2) if peers else None,
+            "GBps_rank_total": round(2 * len(peers) * n * 4 / sec / 1e9, 2) if peers else None,
+            "payload_ok": ok}
+
+
 def _free_port() -> int:
     import socket
 
@@ -862,16 +953,32 @@ def main():
         dev = torch.device("cuda", local_rank % ndev)
         backend = "gt:mi355x"
     dist = None
+    probe = None
     if world > 1 or args.halo_selfcomm:
         from gt4py_amd.distributed import init_process_group
 
+        phase = RankPhase(rank, float(os.environ.get("GTMI_DIST_SETUP_TIMEOUT", "300")))
         # nccl (= RCCL over xGMI) on a real node; GTMI_DIST_BACKEND=gloo rehearses N ranks.
         # Keep RCCL's version banner off stdout: rank 0 prints exactly one JSON line there.
         os.environ.setdefault("NCCL_DEBUG", "WARN")
+        phase.set("init_process_group")
         init_process_group("gloo" if args.dry_run else os.environ.get("GTMI_DIST_BACKEND", "nccl"))
         import torch.distributed as dist
 
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
+        phase.set("first barrier")
+        dist.barrier()
+        phase.set("link probe")
+        dec = None
+        if world > 1 and args.decomp == "2d":
+            from gt4py_amd.distributed import Decomposition2D
+
+            pi = max(p for p in range(1, int(world ** 0.5) + 1) if world % p == 0)
+            dec = Decomposition2D(pi, world // pi, pi, world // pi, (False, False))
+        mine = link_probe(dist, dev, rank, probe_peers(rank, world, dec, args.halo_selfcomm))
+        probe = [None] * world
+        dist.all_gather_object(probe, mine)
+        phase.finish()
 
     box = None
     if not args.dry_run:
@@ -1006,6 +1113,13 @@ def main():
     result["hbm_estimate"] = dict(wl.hbm_estimate, per_rank=True)
     if dist_rec is not None:
         result["dist"] = dist_rec
+    if probe is not None:
+        rates = [r["GBps_per_link_each_way"] for r in probe if r["GBps_per_link_each_way"]]
+        result.setdefault("dist", {})["link_probe"] = {
+            "note": "before the headline: one 10.5 MB message (the C5 f32 J face) to and from each halo peer in "
+                    "one batch_isend_irecv, after a warm-up exchange; per rank",
+            "ranks": probe, "min_GBps_per_link": min(rates) if rates else None,
+            "all_payloads_ok": all(r["payload_ok"] for r in probe)}
     if halo_ab is not None:
         result["halo_ab"] = halo_ab
     if world == 1 and not args.dry_run and not args.halo_selfcomm and args.sustain > 0:

@@ -117,10 +117,7 @@ class Mi355xBackend(BaseBackend):
         "fuse": {"versioning": True, "type": int, "description": "merge adjacent PARALLEL computations over identical intervals into one launch (1, default)"},
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "kreg_pf": {"versioning": True, "type": int, "description": "column kernels: register-band levels whose memory fronts are loaded ahead (default: the load ring depth + 2; 0 = at their level)"},
-        "kreg_pf_span": {"versioning": True, "type": int, "description": "register band: prefetch across section and writer/reader boundaries (1, default) or per section (0)"},
-        "kpf_adapt": {"versioning": True, "type": int, "description": "column kernels: deeper band prefetch and load ring for loops with at most 3 memory operations per level (1; default 0)"},
-        "nbr_shfl": {"versioning": True, "type": int, "description": "column kernels: I-neighbour reads (+-1, 0) of a field also read at (0, 0) from DPP lane shifts plus one wave-uniform edge load (1) or their own loads (0)"},
-        "seg_tail": {"versioning": True, "type": int, "description": "column kernels: run the tail writer's cached and uncached levels as separate segments (1)"},
+        "kbuf": {"versioning": True, "type": int, "description": "column kernels: K-streaming loads/stores through field-wide buffer descriptors (32-bit offsets, no clamps; a 64-bit variant runs for fields past 2 GiB)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},

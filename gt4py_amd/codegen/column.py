@@ -41,24 +41,53 @@ DEFAULT_KREG = -1
 AUTO_KREG = 96  # write-free scratch tails
 AUTO_KREG_API = 48  # tails of API outputs
 AUTO_KREG_API_PF = 6
-# register band fronts prefetched across section and writer/reader boundaries, AUTO_BAND_PF levels
-# ahead (ring depth + 2): vadv 1024^2x160 1.763 ms against 1.800-1.810 (pf 10 per section) and
+# register band fronts prefetched across section and writer/reader boundaries, BAND_PF_OVER_RING
+# levels beyond the ring depth: vadv 1024^2x160 1.763 ms against 1.800-1.810 (pf 10 per section) and
 # 1.791 (pf 12 per section, the round-4 default, which spilled 9 registers); span pf 8 1.780,
-# pf 12 1.791; tridiag -0.3 % (profiles/r04/r04n_sweep_*_span_*.log)
-DEFAULT_BAND_SPAN = 1
+# pf 12 1.791; tridiag -0.3 % (profiles/r04/r04n_sweep_*_span_*.log). Measured and removed in
+# round 5: the per-section prefetch, deeper prefetch for light loops (kpf_adapt),
+# I-neighbour lane shifts (nbr_shfl) and split cached/uncached writer segments (seg_tail).
 BAND_PF_OVER_RING = 2
-# light streams (at most LIGHT_OPS memory operations per level, loads + stores) move too few bytes
-# per level for a 10-level prefetch to cover HBM latency with one wave per SIMD (vadv's backward
-# sweep: one load, one store): option ``kpf_adapt`` deepens their band prefetch and load ring to
-# VM_SLOTS // ops levels (at most ADAPT_MAX); loads and stores share the 6-bit vmcnt
-DEFAULT_PF_ADAPT = 0
-# I-neighbour reads from lane shifts (option ``nbr_shfl``): a field read at (+-1, 0) next to its
-# own column takes the neighbour lane's load (DPP wave rotate) plus one wave-uniform load of the
-# column past the wave, instead of a second, misaligned 64-lane load per level
-DEFAULT_NBR = 0
-LIGHT_OPS = 3
-VM_SLOTS = 48
-ADAPT_MAX = 32
+# K-streaming buffer loads (option ``kbuf``): the kernel is a template over KB; the launch takes
+# KB = true when every field's byte span (plus the look-ahead of speculative levels) fits int32
+DEFAULT_KBUF = 0
+KBUF_HELPERS = [
+    "#ifndef GTMI_KBUF_HELPERS",
+    "#define GTMI_KBUF_HELPERS",
+    "namespace gtmi {",
+    "// a whole field as one buffer: offsets past either end (speculative levels) read 0, stores drop",
+    "GTMI_DEV __amdgpu_buffer_rsrc_t field_rsrc(const void* base, int32_t nbytes) {",
+    "    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);",
+    "}",
+    "template <typename T, bool NT> GTMI_DEV T kload(__amdgpu_buffer_rsrc_t rs, int32_t off) {",
+    "    T v;",
+    "    if constexpr (sizeof(T) == 8) { const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 8); }",
+    "    else if constexpr (sizeof(T) == 4) { const auto x = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 4); }",
+    "    else if constexpr (sizeof(T) == 2) { const auto x = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 2); }",
+    "    else { const auto x = __builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 1); }",
+    "    return v;",
+    "}",
+    "template <typename T, bool NT> GTMI_DEV void kstore(__amdgpu_buffer_rsrc_t rs, int32_t off, T v) {",
+    "    if constexpr (sizeof(T) == 8) { decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 8); __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, NT ? 2 : 0); }",
+    "    else if constexpr (sizeof(T) == 4) { decltype(__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 4); __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, 0, NT ? 2 : 0); }",
+    "    else if constexpr (sizeof(T) == 2) { decltype(__builtin_amdgcn_raw_buffer_load_b16(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 2); __builtin_amdgcn_raw_buffer_store_b16(x, rs, off, 0, NT ? 2 : 0); }",
+    "    else { decltype(__builtin_amdgcn_raw_buffer_load_b8(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 1); __builtin_amdgcn_raw_buffer_store_b8(x, rs, off, 0, NT ? 2 : 0); }",
+    "}",
+    "// KB: the buffer form; else the clamped 64-bit address of the same level",
+    "template <bool KB, typename T, bool NT> GTMI_DEV T kld(__amdgpu_buffer_rsrc_t rs, int32_t lo, int32_t kb, const T* cb,",
+    "                                                     int kk, int klo, int khi, int64_t sK) {",
+    "    if constexpr (KB) return kload<T, NT>(rs, lo + kk * kb);",
+    "    else return sload<T, NT>(cb + (int64_t)clampi(kk, klo, khi) * sK);",
+    "}",
+    "template <bool KB, typename T, bool NT> GTMI_DEV void kst(__amdgpu_buffer_rsrc_t rs, int32_t lo, int32_t kb, T* cb,",
+    "                                                        int kk, int klo, int khi, int64_t sK, T v) {",
+    "    if constexpr (KB) kstore<T, NT>(rs, lo + kk * kb, v);",
+    "    else sstore<T, NT>(cb + (int64_t)clampi(kk, klo, khi) * sK, v);",
+    "}",
+    "}  // namespace gtmi",
+    "#endif",
+    "",
+]
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -105,8 +134,10 @@ class ColumnGen:
                     ilo, ihi, jlo, jhi = max(ilo, a), max(ihi, b), max(jlo, c), max(jhi, d)
         self.ext = (ilo, ihi, jlo, jhi)
         self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
-        self.seg_tail = int(opts.get("seg_tail", 0)) == 1
         self.tile = bool(getattr(kernel, "tile", False))
+        # K-streaming loads/stores through field-wide buffer descriptors (option ``kbuf``): one
+        # 32-bit offset per access instead of a clamped 64-bit address, out-of-range levels read 0
+        self.kbuf = int(opts.get("kbuf", DEFAULT_KBUF)) == 1 and not self.tile
         self.lds = set(getattr(kernel, "lds", ()))
         if self.tile:
             bx, by = self._block()
@@ -116,10 +147,6 @@ class ColumnGen:
             if ti and not 8 <= ti <= bx - ilo - ihi:
                 raise ValueError(f"tile_ti must be in [8, {bx - ilo - ihi}] for IJ extent {self.ext}, got {ti}")
         self.info = {li: self._analyse_loop(li) for li in kernel.loops}
-        self.nbr = {li: self._nbr_plan(li) for li in kernel.loops}
-        if not any(self.nbr.values()) or self._has_while():
-            self.nbr = {li: {} for li in kernel.loops}
-        self.nbr_on = any(self.nbr.values())
         self.kreg = 0
         self.band_pf_default = None
         self.tail = None if self.tile else self._plan_tail()
@@ -245,39 +272,6 @@ class ColumnGen:
                 # cannot carry a value across levels that never run
                 raise UnsupportedStencil(f"register temporary '{name}' read at a K offset across a section gap")
         return _LoopInfo(vl.loop_order != ir.LoopOrder.BACKWARD, direct, win, wnames)
-
-    def _nbr_plan(self, li) -> Dict[Tuple[str, int, int], Tuple[Tuple[str, int, int], int]]:
-        """Window keys ``(name, +-1, 0)`` that the I-neighbour lane shift can serve: a memory field
-        this loop does not write, also read at ``(0, 0)`` with the same window front and a window
-        that covers the neighbour's (so every neighbour entry has its own-column twin)."""
-        out = {}
-        if self.tile or int(self.opts.get("nbr_shfl", DEFAULT_NBR)) not in (1, 2):
-            return out
-        inf = self.info[li]
-        for (name, di, dj), rng in inf.win.items():
-            if dj != 0 or di not in (1, -1) or not self._mem(name) or name in inf.wnames or name in inf.direct:
-                continue
-            base = inf.win.get((name, 0, 0))
-            if base is None or rng[0] < base[0] or rng[1] > base[1]:
-                continue
-            if (rng[1] if inf.fwd else rng[0]) != (base[1] if inf.fwd else base[0]):
-                continue
-            out[(name, di, dj)] = ((name, 0, 0), di)
-        return out
-
-    def _has_while(self) -> bool:
-        """A data-dependent loop in the kernel: lanes past the domain (kept alive for the shuffles)
-        would run it on garbage."""
-        def walk(stmts):
-            for x in stmts:
-                if isinstance(x, ir.While):
-                    return True
-                if isinstance(x, ir.If) and (walk(x.body) or walk(x.orelse or [])):
-                    return True
-                if isinstance(x, ir.HorizontalRegion) and walk(x.body):
-                    return True
-            return False
-        return any(walk(sec.body) for li in self.kernel.loops for sec in self.st.vertical_loops[li].sections)
 
     def _plan_tail(self) -> Optional[_Tail]:
         budget = int(self.opts.get("ktail_lds", LDS_BYTES))
@@ -429,35 +423,12 @@ class ColumnGen:
                 if self._mem(n) and n not in self.scratch and not (read_loops.get(n, set()) - wl)
             }
         scalars = st.scalar_params()
-        L = []
-        if self.nbr_on:
-            # I-neighbour helpers, emitted only by kernels that use them (the device header, which
-            # every library key hashes, stays as it is)
-            L += [
-                "#ifndef GTMI_NBR_HELPERS",
-                "#define GTMI_NBR_HELPERS",
-                "namespace gtmi {",
-                "// a field's value one column over (I + D) from the wave's own loads: lane l takes lane",
-                "// l + D's value; the lane whose neighbour lies in the next (D = 1) or previous (D = -1) wave",
-                "// takes ``edge``, one wave-uniform load of that column. Every lane of the wave must be live.",
-                "template <int D, typename T> GTMI_DEV T nbr(T base, T edge) {",
-                "    const T s = shfl_c<D>(base);",
-                "    const int lane = (int)__lane_id();",
-                "    return (D == 1 ? lane == 63 : lane == 0) ? edge : s;",
-                "}",
-                "// a wave-uniform load of memory the kernel only reads, through the constant address space",
-                "template <typename T> GTMI_DEV T uload(const T* p) {",
-                "    using G = const __attribute__((address_space(1))) T;",
-                "    using C = const __attribute__((address_space(4))) T;",
-                "    return *(C*)(G*)p;",
-                "}",
-                "}  // namespace gtmi",
-                "#endif",
-                "",
-            ]
+        L = list(KBUF_HELPERS) if self.kbuf else []
         L.append(f"struct K{k}Params {{")
         for s in used:
             L += ["    " + x for x in kparam_decl(s, s.name in written)]
+            if self.kbuf:
+                L.append(f"    const void* b_{s.c}; int32_t nb_{s.c};  // the whole field as one buffer (KB)")
         for s in scalars:
             L.append(f"    {s.dtype.ctype} s_{cname(s.name)};")
         L.append("    int32_t ni, nj, nk;")
@@ -465,6 +436,8 @@ class ColumnGen:
         L.append("};")
         L.append("")
         bx, by = self._block()
+        if self.kbuf:
+            L.append("template <bool KB>")
         L.append(f"__global__ void __launch_bounds__({bx * by}) k{k}_column(const K{k}Params p) {{")
         B = []
         eilo, eihi, ejlo, ejhi = self.ext
@@ -501,15 +474,7 @@ class ColumnGen:
             B.append(f"const int i = (int)(blockIdx.x * {bx} + threadIdx.x) - {eilo};")
             B.append(f"const int j = (int)(blockIdx.y * {by} + threadIdx.y) - {ejlo};")
         if not self.tile:
-            if self.nbr_on:
-                # whole waves only (j is wave-uniform): the I-neighbour shuffles need every lane, so
-                # lanes past the domain in I stay, compute on clamped loads and store nothing
-                B.append(f"if (j >= p.nj + {ejhi}) return;")
-                B.append(f"const bool ialive = i < p.ni + {eihi};")
-                B.append("const int gi0_ = __builtin_amdgcn_readfirstlane(i - (int)(threadIdx.x & 63));")
-                B.append("const int gj_ = __builtin_amdgcn_readfirstlane(j);")
-            else:
-                B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
+            B.append(f"if (i >= p.ni + {eihi} || j >= p.nj + {ejhi}) return;")
         B.append("const int nk = p.nk;")
         for s in scalars:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
@@ -527,19 +492,14 @@ class ColumnGen:
                 for acc, w in iter_accesses(sec.body):
                     if isinstance(acc, ir.FieldAccess) and acc.name in inf.direct:
                         self._base(acc.name, acc.offset[0], acc.offset[1], B, acc.name in written)
-        # I-neighbour edges: the one column past the wave (D = 1) or before it (D = -1), wave-uniform
-        self.edge_bases: Dict[Tuple[str, int], str] = {}
-        for li in self.kernel.loops:
-            for (name, di, _dj) in self.nbr[li]:
-                if (name, di) in self.edge_bases:
-                    continue
-                c = cname(name)
-                v = f"ce_{c}_{_sgn(di)}"
-                t = self.st.decl(name).dtype.ctype
-                col = "gi0_ + 64" if di == 1 else "gi0_ - 1"
-                B.append(f"const {t}* __restrict__ {v} = p.p_{c} + ((int64_t)gtmi::clampi({col}, p.ilo_{c}, p.ihi_{c}) * "
-                         f"p.sI_{c} + (int64_t)gtmi::clampi(gj_, p.jlo_{c}, p.jhi_{c}) * p.sJ_{c});")
-                self.edge_bases[(name, di)] = v
+        if self.kbuf:
+            # one descriptor per field (wave-uniform: kernel arguments only), the level stride in
+            # bytes, and each column base as a byte offset into the field's buffer
+            for s in used:
+                B.append(f"const __amdgpu_buffer_rsrc_t rs_{s.c} = gtmi::field_rsrc(p.b_{s.c}, KB ? p.nb_{s.c} : 0);")
+                B.append(f"const int32_t kb_{s.c} = (int32_t)p.sK_{s.c} * (int32_t)sizeof(*p.p_{s.c});")
+            for (name, di, dj), v in list(self.bases.items()):
+                B.append(f"const int32_t lo_{v[3:]} = KB ? (int32_t)((const char*){v} - (const char*)p.b_{cname(name)}) : 0;")
         if self.tail is not None:
             t = self.tail
             B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
@@ -563,11 +523,11 @@ class ColumnGen:
                 ct = self.st.decl(n).dtype.ctype
                 B.append(f"{ct}* __restrict__ {t.var(n)} = ({ct}*)(gtmi_lds + {off});")
                 off = f"{off} + (size_t)p.tail_len * 256 * sizeof({ct})"
-        # prefetch across the writer/reader boundary of the register band (kreg_pf_span): the
+        # prefetch across the writer/reader boundary of the register band: the
         # reader is rendered first so that the writer's last band levels can issue the reader's
         # first band prefetches (declared here, at kernel scope)
         t_ = self.tail
-        self._xpf = bool(self.kreg) and int(self.opts.get("kreg_pf_span", DEFAULT_BAND_SPAN)) == 1 and t_ is not None \
+        self._xpf = bool(self.kreg) and t_ is not None \
             and t_.a != t_.b and t_.b in self.kernel.loops and t_.a in self.kernel.loops \
             and self.kernel.loops.index(t_.b) == self.kernel.loops.index(t_.a) + 1
         if self._xpf:
@@ -598,8 +558,9 @@ class ColumnGen:
             lds = f"(size_t)p.tail_len * {self.tail_per_level}"
             H.append("        static bool lds_attr = false;")
             H.append("        if (!lds_attr) {")
-            H.append(f"            hipFuncSetAttribute((const void*)k{k}_column, hipFuncAttributeMaxDynamicSharedMemorySize, "
-                     f"{LDS_BYTES});")
+            for inst in ((f"k{k}_column<true>", f"k{k}_column<false>") if self.kbuf else (f"k{k}_column",)):
+                H.append(f"            hipFuncSetAttribute((const void*){inst}, hipFuncAttributeMaxDynamicSharedMemorySize, "
+                         f"{LDS_BYTES});")
             H.append("            lds_attr = true;")
             H.append("        }")
         else:
@@ -611,10 +572,27 @@ class ColumnGen:
                 f"(unsigned)((nj + {TJ - 1}) / {TJ})), dim3({bx}, {by}), {lds}, stream, p);"
             )
         else:
-            H.append(
-                f"        hipLaunchKernelGGL(k{k}_column, dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
-                f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p);"
-            )
+            grid = (f"dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
+                    f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p")
+            if self.kbuf:
+                # KB when every field's bytes, plus the speculative levels the rings and band
+                # prefetches reach past either end, fit a signed 32-bit offset
+                look = self.ring + max(self.kreg, 0) + 2 + max((abs(d) for inf in self.info.values()
+                                                                for rng in inf.win.values() for d in rng), default=0)
+                H.append("        bool kb_ok = true;")
+                for s in used:
+                    q = f"f[{s.index}]"
+                    H.append(f"        {{  int64_t span = 1; for (int d = 0; d < 3; ++d) span += ({q}.shape[d] - 1) * {q}.strides[d];")
+                    H.append(f"           for (int d = 0; d < {q}.n_data_dims; ++d) span += ({q}.data_shape[d] - 1) * {q}.data_strides[d];")
+                    H.append(f"           const int64_t isz = (int64_t)sizeof(*p.p_{s.c}), nb = span * isz;")
+                    H.append(f"           const int64_t reach = nb + (int64_t)(nk + {look}) * (p.sK_{s.c} < 0 ? -p.sK_{s.c} : p.sK_{s.c}) * isz;")
+                    H.append(f"           bool pos = true; for (int d = 0; d < 3; ++d) pos = pos && {q}.strides[d] >= 0;")
+                    H.append(f"           kb_ok = kb_ok && pos && reach < ((int64_t)1 << 31);")
+                    H.append(f"           p.b_{s.c} = {q}.data; p.nb_{s.c} = (int32_t)(nb < ((int64_t)1 << 31) ? nb : 0); }}")
+                H.append(f"        if (kb_ok) hipLaunchKernelGGL(k{k}_column<true>, {grid});")
+                H.append(f"        else hipLaunchKernelGGL(k{k}_column<false>, {grid});")
+            else:
+                H.append(f"        hipLaunchKernelGGL(k{k}_column, {grid});")
         H.append("    }")
         H.append("}")
         return "\n".join(L), "\n".join(H)
@@ -660,25 +638,14 @@ class ColumnGen:
             c = cname(name)
             return f"({self.bases[(name, di, dj)]} + (int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
 
-        derived = self.nbr.get(li, {})
-
         def mem_index(name, di, dj, kexpr):
-            """A load expression (non-temporal for read-once streams). For an I-neighbour key the
-            lane shift serves (``derived``) it is the wave-uniform edge load only; see ``nbr_of``."""
-            if (name, di, dj) in derived:
-                c = cname(name)
-                ptr = f"({self.edge_bases[(name, di)]} + (int64_t)gtmi::clampi({kexpr}, p.klo_{c}, p.khi_{c}) * p.sK_{c})"
-                if int(self.opts.get("nbr_shfl", DEFAULT_NBR)) == 2:  # vector load, uniform address
-                    return f"gtmi::sload<{decl_dtype[name].ctype}, false>({ptr})"
-                return f"gtmi::uload<{decl_dtype[name].ctype}>({ptr})"
+            """A load expression (non-temporal for read-once streams)."""
             nt = "true" if (name in self.nt_loads and name not in direct) else "false"
+            if self.kbuf and name not in direct:
+                c, v = cname(name), self.bases[(name, di, dj)]
+                return (f"gtmi::kld<KB, {decl_dtype[name].ctype}, {nt}>(rs_{c}, lo_{v[3:]}, kb_{c}, {v}, {kexpr}, "
+                        f"p.klo_{c}, p.khi_{c}, p.sK_{c})")
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
-
-        def nbr_of(key, d, edge):
-            """Window entry ``d`` of I-neighbour key ``key``: the own-column entry of the neighbour
-            lane, the wave's edge column from ``edge``."""
-            (bname, bdi, bdj), D = derived[key]
-            return f"gtmi::nbr<{D}>({wvar(bname, bdi, bdj, d)}, {edge})"
 
         def load_into(var, name, di, dj, kexpr, maybe_cached=True, reg=None) -> List[str]:
             """``var = F(level kexpr)``: from the LDS tail cache when this loop reads a cached level
@@ -699,7 +666,12 @@ class ColumnGen:
 
         def mem_store(name, kexpr, value):
             nt = "true" if (name in self.nt_stores and name not in direct) else "false"
-            st = f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
+            if self.kbuf and name not in direct:
+                c, v = cname(name), self.bases[(name, 0, 0)]
+                st = (f"gtmi::kst<KB, {decl_dtype[name].ctype}, {nt}>(rs_{c}, lo_{v[3:]}, kb_{c}, {v}, {kexpr}, "
+                      f"p.klo_{c}, p.khi_{c}, p.sK_{c}, {value});")
+            else:
+                st = f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
             if name in no_store and kexpr == "k":
                 if band_now[0] == "reg":
                     return "// register band level: kept in registers only"
@@ -707,8 +679,6 @@ class ColumnGen:
                     return "// cached level: kept in LDS only"
                 if band_now[0] is None:
                     st = f"if (k < tc0 || k >= tc1) {st}"
-            if self.nbr_on:
-                st = f"if (ialive) {st}"
             return st
 
         P = self.ring
@@ -760,14 +730,11 @@ class ColumnGen:
 
         sec_start = len(out)
         band_code: List[str] = []
-        # register band fronts prefetched across the whole band (option ``kreg_pf_span``): one
-        # sweep-order list of band levels over all sections, each level prefetching the one ``Pb``
-        # levels on whatever section it lies in, and -- for the writer, whose band ends the sweep
-        # -- the prologue issued at the start of the loop, so no band level (nor the first) waits
-        # for loads issued at a section boundary
-        span = bool(R) and int(self.opts.get("kreg_pf_span", DEFAULT_BAND_SPAN)) == 1
-        # memory fields this loop stores at every level (the band's no-store scratch aside)
-        loop_stores = {n for n in wnames if self._mem(n) and n not in direct and n not in no_store}
+        # register band fronts prefetched across the whole band: one sweep-order list of band
+        # levels over all sections, each level prefetching the one ``Pb`` levels on whatever
+        # section it lies in, and -- for the writer, whose band ends the sweep -- the prologue
+        # issued at the start of the loop, so no band level (nor the first) waits for loads issued
+        # at a section boundary
         if R:
             Pb = int(self.opts.get("kreg_pf", self.band_pf_default if self.band_pf_default is not None else P + BAND_PF_OVER_RING))
             kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
@@ -785,10 +752,6 @@ class ColumnGen:
                     mk.append(key)
                 mem_keys[u] = mk
             pfv = {}
-            if int(self.opts.get("kpf_adapt", DEFAULT_PF_ADAPT)) == 1 and "kreg_pf" not in self.opts and all_us:
-                n_ops = max(len(mem_keys[u]) for u in all_us) + len(loop_stores)
-                if 0 < n_ops <= LIGHT_OPS:
-                    Pb = max(Pb, min(ADAPT_MAX, VM_SLOTS // n_ops))
 
             def prefetch(u_):
                 return [f"{pfv[(u_, key)]} = {mem_index(key[0], key[1], key[2], f'({kexpr_of(u_)}) + ({front[key]})')};"
@@ -807,7 +770,7 @@ class ColumnGen:
             # registers afford); the rest are issued at most two per level, each ``Pb`` levels
             # ahead or as early as that allows, so a deeper distance ramps up within the band
             issue_at: Dict[int, List[int]] = {}
-            if span and Pb > 0:
+            if Pb > 0:
                 pre = Pb
                 if self._xpf and li == tail.b:
                     pre = min(Pb, int(self.opts.get("kreg_pf", P + BAND_PF_OVER_RING)))
@@ -816,13 +779,13 @@ class ColumnGen:
                 for p_ in range(len(all_us)):
                     while pend and pend[0] - Pb <= p_ and len(issue_at.get(p_, ())) < 2:
                         issue_at.setdefault(p_, []).append(pend.pop(0))
-            if span and Pb > 0 and self._xpf and li == tail.b:
+            if Pb > 0 and self._xpf and li == tail.b:
                 # reader: its first ``pre`` band levels are prefetched by the writer's last band levels
                 self._xpf_decls = declare_pf(all_us[:pre], "")
                 self._xpf_loads = [prefetch(u) for u in all_us[:pre]]
                 out += declare_pf(all_us[pre:], "    ")
                 sec_start = len(out)
-            elif span and Pb > 0:
+            elif Pb > 0:
                 out += declare_pf(all_us, "    ")
                 out.append("    if (regband) {  // band prefetch prologue (whole band)")
                 for u in all_us[:pre]:
@@ -864,7 +827,7 @@ class ColumnGen:
                 index), from a band prefetch register (``pf``: key -> variable) or from memory here
                 (``slot`` None)."""
                 body = []
-                for key, rng in sorted(win.items(), key=lambda kv: kv[0] in derived):
+                for key, rng in win.items():
                     name, di, dj = key
                     ds = list(range(rng[0], rng[1] + 1))
                     if fwd:
@@ -873,17 +836,7 @@ class ColumnGen:
                     else:
                         for d in reversed(ds[1:]):
                             body.append(f"{wvar(name, di, dj, d)} = {wvar(name, di, dj, d - 1)};")
-                    if front_load[key] and key in derived:
-                        fd = front[key]
-                        fv = wvar(name, di, dj, fd)
-                        if pf is not None and key in pf:
-                            edge = pf[key]
-                        elif slot is not None and key in ring_keys and reg_u is None:
-                            edge = f"rg{slot}_{fv}"
-                        else:
-                            edge = mem_index(name, di, dj, f"k + ({fd})")
-                        body.append(f"{fv} = {nbr_of(key, fd, edge)};")
-                    elif front_load[key]:
+                    if front_load[key]:
                         fd = front[key]
                         fv = wvar(name, di, dj, fd)
                         if pf is not None and key in pf:
@@ -900,17 +853,11 @@ class ColumnGen:
 
             def reload(reg_u: Optional[int] = None, pf: Optional[Dict] = None) -> List[str]:
                 body = []
-                for (name, di, dj), rng in sorted(win.items(), key=lambda kv: kv[0] in derived):
+                for (name, di, dj), rng in win.items():
                     if not self._mem(name):
                         continue
                     for d in range(rng[0], rng[1] + 1):
                         if d == 0 and not zero_needed_in(name, di, dj, sec):
-                            continue
-                        if (name, di, dj) in derived:
-                            key_ = (name, di, dj)
-                            edge = pf[key_] if (pf is not None and key_ in pf and d == front[key_]) else \
-                                mem_index(name, di, dj, f"k + ({d})")
-                            body.append(f"{wvar(name, di, dj, d)} = {nbr_of(key_, d, edge)};")
                             continue
                         if pf is not None and (name, di, dj) in pf and d == front[(name, di, dj)]:
                             body.append(f"{wvar(name, di, dj, d)} = {pf[(name, di, dj)]};")  # prefetched
@@ -976,12 +923,7 @@ class ColumnGen:
                 """Levels [ss, se) of the section in sweep order. ``mode``: "mem" (no front of
                 these levels is tail-cached), "lds" (every tail-cached front is), "mixed"."""
                 keys = [k_ for k_ in ring_keys if not (mode == "lds" and k_ in tail_keys)] if mode != "mixed" else []
-                Pseg = P
-                if keys and int(self.opts.get("kpf_adapt", DEFAULT_PF_ADAPT)) == 1 and "kring" not in self.opts:
-                    n_ops = len(keys) + len(loop_stores)
-                    if n_ops <= LIGHT_OPS:
-                        Pseg = max(P, min(ADAPT_MAX, VM_SLOTS // n_ops))
-                R = _section_ring(sec.interval, Pseg) if keys else 0
+                R = _section_ring(sec.interval, P) if keys else 0
                 o = [f"{{  // levels [{ss}, {se}), {mode}"]
                 o.append(f"    const int ss = {ss}, se = {se};")
                 first = "ss" if fwd else "se - 1"
@@ -1043,18 +985,7 @@ class ColumnGen:
                 o.append("}")
                 return o
 
-            if tail_write and self.seg_tail:
-                # tail writer: the levels before the cached band (in sweep order) and the band
-                # itself run as separate segments, so no level tests whether it is cached
-                if fwd:
-                    parts = [("ks", "(ke < tc0 ? ke : tc0)", False), ("(ks > tc0 ? ks : tc0)", "ke", True)]
-                else:
-                    parts = [("(ks > tc1 ? ks : tc1)", "ke", False), ("ks", "(ke < tc1 ? ke : tc1)", True)]
-                for ss, se, band in parts:
-                    band_now[0] = band
-                    out += ["        " + x for x in segment(ss, se, "mem")]
-                band_now[0] = None
-            elif tail_keys:
+            if tail_keys:
                 # split the section by where the tail-cached fronts come from. A front k + fd is
                 # cached iff tc0 <= k + fd < tc1. With lo/hi the smallest/largest fd of the tail keys:
                 # all fronts cached for k in [tc0 - lo, tc1 - hi), none below tc0 - hi or from
@@ -1087,31 +1018,22 @@ class ColumnGen:
                 # band level n's fronts are loaded ``kreg_pf`` band levels earlier into registers
                 # of their own (a level waiting for its own loads stalls a one-wave-per-SIMD kernel)
                 order_us = sorted(us, reverse=not fwd)
-                # prefetch distance: see BAND_PF_OVER_RING (per-section prologues, before the span:
-                # pf 8 1.854, 12 1.822, 16 1.914, 24 2.159 ms; profiles/r04/sweep_vadv_band_pf.log)
+                # prefetch distance: see BAND_PF_OVER_RING
                 bc = [f"    if (regband) {{  // section {si}: register band levels"]
-                if Pb > 0 and not span:
-                    bc += declare_pf(order_us, "        ")
-                    bc.append("        // band prefetch prologue")
-                    for u in order_us[:Pb]:
-                        bc += ["        " + x for x in prefetch(u)]
-                seq = all_us if span else order_us
+                seq = all_us
                 for n_, u in enumerate(order_us):
                     kexpr = kexpr_of(u)
                     reg_now[0], band_now[0] = u, "reg"
                     pf = {key: pfv[(u, key)] for key in mem_keys[u]} if Pb > 0 else None
                     if n_ == 0:
-                        body = (["if (k != k_next) {"] + ["    " + x for x in reload(u, pf if span else None)] + ["} else {"]
+                        body = (["if (k != k_next) {"] + ["    " + x for x in reload(u, pf)] + ["} else {"]
                                 + ["    " + x for x in shift_and_fronts(None, "mem", u, pf)] + ["}"])
                     else:
                         body = shift_and_fronts(None, "mem", u, pf)
                     g_ = seq.index(u)
-                    if span:
-                        for t_ in issue_at.get(g_, ()):
-                            body += prefetch(seq[t_])
-                    elif Pb > 0 and g_ + Pb < len(seq):
-                        body += prefetch(seq[g_ + Pb])
-                    if span and self._xpf and li == tail.a and Pb > 0:
+                    for t_ in issue_at.get(g_, ()):
+                        body += prefetch(seq[t_])
+                    if self._xpf and li == tail.a and Pb > 0:
                         # the reader's band level j is prefetched its own distance (len(_xpf_loads))
                         # before the reader starts
                         j_ = g_ + len(self._xpf_loads) - len(seq)

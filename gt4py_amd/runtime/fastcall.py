@@ -57,10 +57,17 @@ def _digest() -> str:
         with open(p, "rb") as f:
             h.update(f.read())
     h.update(torch.__version__.encode())
-    # the command with the repository's own paths made relative: the tree is built here and run
-    # from another directory on the GPU box
-    repo = os.path.dirname(_PKG)
-    h.update(" ".join(c.replace(repo, "<repo>") for c in _command(target_path())).encode())
+    # the command (flags, C++ ABI) with every installation prefix replaced by its role: the tree
+    # is built here and run from another directory on the GPU box, whose torch and Python may
+    # live under other prefixes
+    prefixes = [(os.path.dirname(_PKG), "<repo>"), (os.path.dirname(os.path.abspath(torch.__file__)), "<torch>"),
+                (sysconfig.get_paths()["include"], "<python-include>"), ("/opt/rocm", "<rocm>")]
+    cmd = []
+    for c in _command(target_path()):
+        for pre, role in prefixes:
+            c = c.replace(pre, role)
+        cmd.append(c)
+    h.update(" ".join(cmd).encode())
     return h.hexdigest()[:24]
 
 
@@ -94,7 +101,7 @@ def build(verbose: bool = False) -> str:
 def module():
     """The extension module, or None if it is not built, is stale (built from other sources, for
     another torch or with other flags) or fails to import -- the launcher then uses its ctypes
-    closure, with a warning for the last two cases."""
+    closure, with a warning for the last two cases. Stale under ``GTMI_NO_COMPILE`` raises."""
     global _module, _tried
     if not _tried:
         _tried = True
@@ -105,6 +112,11 @@ def module():
             import torch  # noqa: F401  (its libraries first)
 
             if not up_to_date():
+                if os.environ.get("GTMI_NO_COMPILE"):
+                    # a run that may not compile must not quietly measure the slower ctypes path
+                    _tried = False
+                    raise RuntimeError(f"{target_path()} is stale and GTMI_NO_COMPILE is set: rebuild it with "
+                                       "gt4py_amd.runtime.fastcall.build() (or set GTMI_FASTCALL=0)")
                 warnings.warn(f"{target_path()} is stale (rebuild with gt4py_amd.runtime.fastcall.build()); "
                               "using the ctypes launch path", RuntimeWarning, stacklevel=2)
                 return None

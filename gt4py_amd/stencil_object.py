@@ -95,10 +95,20 @@ def _nt_le(a, b) -> bool:
 _FAST_MEMO_MAX = 64
 _FAST_SIGS_PER_ARGS = 8
 
-# every prepared-launch memo (per StencilObject class, per FrozenStencil): they hold weak
-# references to the argument tensors (drop_prepared_launches)
-_CLASS_MEMOS: list = []
+# every StencilObject class with a prepared-launch memo (``_gt_fast_memo_``; the memos hold weak
+# references to the argument tensors, drop_prepared_launches). Weak: a class that is no longer
+# used takes its memo, closures and packed arguments with it
+_MEMO_CLASSES = None
 _FROZEN = None  # id -> FrozenStencil (weak values; frozen stencils are not hashable), made on first use
+
+
+def _memo_classes():
+    global _MEMO_CLASSES
+    if _MEMO_CLASSES is None:
+        import weakref
+
+        _MEMO_CLASSES = weakref.WeakSet()
+    return _MEMO_CLASSES
 
 
 def _frozen_set():
@@ -114,8 +124,8 @@ def drop_prepared_launches() -> None:
     """Forget every prepared launch and packed argument array (they hold weak references to and
     borrowed pointers of the argument tensors): the next call of each signature prepares it
     again. Used before tensors are re-homed in place (``storage.placement.tune_in_place``)."""
-    for memo in _CLASS_MEMOS:
-        memo.clear()
+    for cls in list(_memo_classes()):
+        cls._gt_fast_memo_.clear()
     for fz in list(_frozen_set().values()):
         fz._memo.clear()
     from gt4py_amd.runtime.launcher import drop_pack_caches
@@ -710,7 +720,6 @@ def make_stencil_class(
     pdict = ", ".join(f"{n}={n}" for n in param_names)
     # fast path (see _fast_tensors): id tuple -> [(domain, origin, prepared launch(fields, params) -> bool)]
     memo: Dict[tuple, tuple] = {}
-    _CLASS_MEMOS.append(memo)
     ns["_memo"] = memo
     src = (
         f"def __call__(self, {', '.join(parts)}):\n"
@@ -751,4 +760,6 @@ def make_stencil_class(
         "_instance": None,
         "_gt_fast_memo_": memo,
     }
-    return type(class_name, (StencilObject,), attrs)
+    cls = type(class_name, (StencilObject,), attrs)
+    _memo_classes().add(cls)
+    return cls

@@ -216,8 +216,8 @@ def tune_in_place(
     ``"in_place": True``).
 
     Raises ``ValueError`` (before anything is timed) for a written field that other tensors view
-    (they would keep the old pages) and ``RuntimeError`` if a field is weakly referenced outside
-    gt4py_amd; gt4py_amd's own prepared launches and packed-argument caches are dropped first
+    (they would keep the old pages) and ``RuntimeError`` (also before timing) if a field is weakly
+    referenced outside gt4py_amd; gt4py_amd's own prepared launches and packed-argument caches are dropped first
     (they hold weak references and borrowed pointers; the next call re-prepares them).
     """
     import torch
@@ -230,15 +230,22 @@ def tune_in_place(
         if not _exclusive(t):
             raise ValueError(f"tune_placement: written field '{n}' shares its storage with other tensors "
                              f"(views would keep the old buffer); use tune_written_fields and pass the returned arrays")
+    # weak references held outside gt4py_amd: refused before anything is timed (our own prepared
+    # launches and packed-argument caches are dropped first; they re-prepare on the next call)
+    import weakref
+
+    from gt4py_amd.stencil_object import drop_prepared_launches
+
+    drop_prepared_launches()
+    held = [n for n in names if weakref.getweakrefcount(arrays[n])]
+    if held:
+        raise RuntimeError(f"tune_placement: field(s) {held} are weakly referenced elsewhere; cannot re-home "
+                           "them in place (use tune_written_fields)")
     out, report = tune_written_fields(stencil, arrays, origin=origin, domain=domain, params=params,
                                       candidates=candidates, reps=reps, memory_fraction=memory_fraction)
     moved = [n for n in names if out[n] is not arrays[n]]
     if moved:
-        import weakref
-
-        from gt4py_amd.stencil_object import drop_prepared_launches
-
-        drop_prepared_launches()
+        drop_prepared_launches()  # the tuner's own timing calls prepared launches again
         held = [n for n in moved if weakref.getweakrefcount(arrays[n])]
         if held:
             raise RuntimeError(f"tune_placement: field(s) {held} are weakly referenced elsewhere; cannot re-home "

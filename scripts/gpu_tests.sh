@@ -4,6 +4,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+# every library key the run requests (tests/gpu_build_keys.txt is made from it; tests/test_prebuild.py)
+export GTMI_CACHE_LOG=${GTMI_CACHE_LOG:-$PWD/gpurun_out/build_keys.log}
 timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests/ ${PYTEST_SEL:-} -x -v -m gpu --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -5

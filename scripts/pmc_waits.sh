@@ -1,0 +1,27 @@
+#!/bin/bash
+# Where the wave cycles go: per config one rocprofv3 pass each of
+#   A  SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES
+#   B  TCC_HIT_sum TCC_MISS_sum
+#   C  SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE
+# (separate passes; WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, MI355X_MICROARCH.md
+# "rocprofv3 PMC slots"), then scripts/summarize_waits.py prints the split per config.
+# Usage: CONFIGS="vadv copy" TAG=r05a [BENCH_OPTS="--opt kbuf=1"] bash scripts/pmc_waits.sh
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r05}
+OUT=gpurun_out/waits_${TAG}
+mkdir -p $OUT
+PASS_A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES"
+PASS_B="TCC_HIT_sum TCC_MISS_sum"
+PASS_C="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+for cfg in ${CONFIGS:-vadv copy}; do
+  for p in A B C; do
+    eval "ctrs=\$PASS_$p"
+    echo "== $cfg pass $p: $ctrs"
+    timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/${cfg}_$p -o pmc -- \
+      python3 bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-extra --placement-candidates 0 ${BENCH_OPTS:-} \
+      > $OUT/${cfg}_$p.log 2>&1 || { tail -20 $OUT/${cfg}_$p.log; exit 1; }
+  done
+done
+python3 scripts/summarize_waits.py $OUT ${CONFIGS:-vadv copy} | tee $OUT/summary.json

@@ -31,3 +31,18 @@ if os.environ.get("GTMI_PREBUILD_TESTS"):
         raise RuntimeError("GTMI_PREBUILD_TESTS: built, not launched")
 
     _gt_launcher.StencilLauncher.__call__ = _no_launch
+
+    _REPORT = os.environ.get("GTMI_PREBUILD_REPORT")
+
+    @pytest.hookimpl(hookwrapper=True)
+    def pytest_runtest_makereport(item, call):
+        outcome = yield
+        rep = outcome.get_result()
+        if _REPORT and rep.when == "call":
+            import json
+
+            err = None
+            if call.excinfo is not None:
+                err = [call.excinfo.type.__name__, str(call.excinfo.value).splitlines()[0][:300] if str(call.excinfo.value) else ""]
+            with open(_REPORT, "a") as f:
+                f.write(json.dumps({"test": item.nodeid, "outcome": rep.outcome, "error": err}) + "\n")

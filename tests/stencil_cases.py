@@ -2202,7 +2202,7 @@ def band_ij_accumulator(a: F64, b: F64, out: F64, s: F2D, lev: Field[IJ, np.int3
 
 def band_ij_accumulator_reader(a: F64, b: F64, out: F64, s: F2D):
     """As ``band_ij_accumulator`` with the IJ accumulator in the reader only, so the writer's last
-    band levels prefetch the reader's first ones (kreg_pf_span across the loop boundary)."""
+    band levels prefetch the reader's first ones (the band's prefetch crosses the loop boundary)."""
     with computation(FORWARD):
         with interval(0, 1):
             c = a

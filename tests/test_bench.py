@@ -60,10 +60,36 @@ def test_bench_launcher_dry_run(gpus, decomp):
         assert "error" not in c5, c5
         assert c5["n_gpus"] == gpus and c5["global_domain"][0] * c5["global_domain"][1] == 64 * 32 * gpus
         assert c5["Mcells_s"] > 0 and c5["scaling"] == "weak"
+        # the link probe ran before the headline: one face-sized message to and from each peer
+        lp = d["link_probe"]
+        assert [r["rank"] for r in lp["ranks"]] == list(range(gpus)) and lp["all_payloads_ok"]
+        for r in lp["ranks"]:
+            assert r["bytes_per_message"] == 10_485_760 and r["peers"] and r["rank"] not in r["peers"]
+            assert r["ms"] > 0 and r["GBps_per_link_each_way"] > 0
+            if decomp == "jstrips":
+                assert r["peers"] == [p for p in (r["rank"] - 1, r["rank"] + 1) if 0 <= p < gpus]
+        assert lp["min_GBps_per_link"] > 0
     else:
         assert "dist" not in rec
     for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "roofline", "config"):
         assert key in rec
+
+
+def test_rank_setup_timeout_names_the_phase():
+    """A rank that cannot finish process-group set-up exits non-zero with its last phase (here:
+    rank 1 of a 2-rank rendezvous never starts, so rank 0 waits in init_process_group)."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    res = _run(["--dry-run", "--gpus", "2", "--steps", "1", "--warmup", "0"],
+               env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                          "MASTER_PORT": str(port), "GTMI_DIST_SETUP_TIMEOUT": "5", "GTMI_DIST_TIMEOUT": "120"},
+               timeout=120)
+    assert res.returncode == 3, (res.returncode, res.stderr[-2000:])
+    assert "no progress past phase 'init_process_group'" in res.stderr
 
 
 def test_bench_world_size_mismatch_is_an_error():

@@ -129,7 +129,7 @@ def test_row_unroll_auto_rule():
         assert ("// slot copy 0" in src) == slots, name
 
 
-@pytest.mark.parametrize("opts", [{}, {"kreg_pf_span": 0}, {"kreg": 40, "kreg_pf": 50}])
+@pytest.mark.parametrize("opts", [{}, {"kreg": 48, "kreg_pf": 6}, {"kreg": 40, "kreg_pf": 50}])
 @pytest.mark.parametrize("name", ["band_ij_accumulator", "band_ij_accumulator_reader"])
 def test_register_band_never_prefetches_written_ij_fields(name, opts):
     """A field a loop both reads and writes that has no K axis (an IJ accumulator) is one address
