@@ -577,18 +577,26 @@ class ColumnGen:
             if self.kbuf:
                 # KB when every field's bytes, plus the speculative levels the rings and band
                 # prefetches reach past either end, fit a signed 32-bit offset
-                look = self.ring + max(self.kreg, 0) + 2 + max((abs(d) for inf in self.info.values()
-                                                                for rng in inf.win.values() for d in rng), default=0)
+                # (the ring reaches kring levels past a section's end; the register band's
+                # prefetches stay inside [0, nk); window offsets add their own reach)
+                look = self.ring + 2 + max((abs(d) for inf in self.info.values() for rng in inf.win.values()
+                                            for d in rng), default=0)
                 H.append("        bool kb_ok = true;")
+                # timing probe only (option ``kbuf_null``: comma-separated fields or "*"): those
+                # fields' descriptors get zero records, so the same instruction stream runs without
+                # their memory traffic (cdna_hip_programming.md, "price ONE buffer's traffic")
+                nl = str(self.opts.get("kbuf_null", ""))
+                null = {s_.name for s_ in used} if nl == "*" else set(filter(None, nl.split(":")))
                 for s in used:
                     q = f"f[{s.index}]"
                     H.append(f"        {{  int64_t span = 1; for (int d = 0; d < 3; ++d) span += ({q}.shape[d] - 1) * {q}.strides[d];")
                     H.append(f"           for (int d = 0; d < {q}.n_data_dims; ++d) span += ({q}.data_shape[d] - 1) * {q}.data_strides[d];")
                     H.append(f"           const int64_t isz = (int64_t)sizeof(*p.p_{s.c}), nb = span * isz;")
-                    H.append(f"           const int64_t reach = nb + (int64_t)(nk + {look}) * (p.sK_{s.c} < 0 ? -p.sK_{s.c} : p.sK_{s.c}) * isz;")
+                    H.append(f"           const int64_t reach = nb + (int64_t){look} * (p.sK_{s.c} < 0 ? -p.sK_{s.c} : p.sK_{s.c}) * isz;")
                     H.append(f"           bool pos = true; for (int d = 0; d < 3; ++d) pos = pos && {q}.strides[d] >= 0;")
                     H.append(f"           kb_ok = kb_ok && pos && reach < ((int64_t)1 << 31);")
-                    H.append(f"           p.b_{s.c} = {q}.data; p.nb_{s.c} = (int32_t)(nb < ((int64_t)1 << 31) ? nb : 0); }}")
+                    nb_expr = "0" if str(s.name) in null else f"(int32_t)(nb < ((int64_t)1 << 31) ? nb : 0)"
+                    H.append(f"           p.b_{s.c} = {q}.data; p.nb_{s.c} = {nb_expr}; }}")
                 H.append(f"        if (kb_ok) hipLaunchKernelGGL(k{k}_column<true>, {grid});")
                 H.append(f"        else hipLaunchKernelGGL(k{k}_column<false>, {grid});")
             else:

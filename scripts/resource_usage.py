@@ -24,15 +24,14 @@ def main():
         opts[k] = int(v)
     sname, dtype, _, _, _ = bench.CONFIGS[cfg]
     from gt4py_amd.backend.base import from_name
-    from gt4py_amd.codegen import hip as hipgen
-    from gt4py_amd.codegen.plan import make_plan
+    from gt4py_amd.backend.mi355x_backend import generate_source
     from gt4py_amd.definitions import BuildOptions
     from gt4py_amd.loader import StencilBuilder
 
     b = StencilBuilder(bench.stencil_defs()[(sname, dtype)], from_name("gt:mi355x"),
                        BuildOptions(name=f"resources.{cfg}", module="resources", backend_opts=opts),
                        bench.EXTERNALS.get(sname, {}), {})
-    source, _ = hipgen.generate(b.analysis, make_plan(b.analysis), opts)
+    _, source, _ = generate_source(b.analysis, opts)  # the backend's own lowering chain
     lib = jit.compile_source(source)
     src = os.path.join(os.path.dirname(lib), "stencil.hip")
     cmd = [jit.hipcc_path()] + jit.BASE_FLAGS + [f"-I{jit.CSRC_DIR}", f"-I{jit.INCLUDE_DIR}",
