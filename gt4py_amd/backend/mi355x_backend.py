@@ -117,8 +117,6 @@ class Mi355xBackend(BaseBackend):
         "fuse": {"versioning": True, "type": int, "description": "merge adjacent PARALLEL computations over identical intervals into one launch (1, default)"},
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "kreg_pf": {"versioning": True, "type": int, "description": "column kernels: register-band levels whose memory fronts are loaded ahead (default: the load ring depth + 2; 0 = at their level)"},
-        "kbuf": {"versioning": True, "type": int, "description": "column kernels: K-streaming loads/stores through field-wide buffer descriptors (32-bit offsets, no clamps; a 64-bit variant runs for fields past 2 GiB)"},
-        "kbuf_null": {"versioning": True, "type": str, "description": "timing probe: fields (':'-separated, '*' = all) whose kbuf descriptors get zero records (no memory traffic, wrong results)"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},

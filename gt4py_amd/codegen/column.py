@@ -48,46 +48,6 @@ AUTO_KREG_API_PF = 6
 # round 5: the per-section prefetch, deeper prefetch for light loops (kpf_adapt),
 # I-neighbour lane shifts (nbr_shfl) and split cached/uncached writer segments (seg_tail).
 BAND_PF_OVER_RING = 2
-# K-streaming buffer loads (option ``kbuf``): the kernel is a template over KB; the launch takes
-# KB = true when every field's byte span (plus the look-ahead of speculative levels) fits int32
-DEFAULT_KBUF = 0
-KBUF_HELPERS = [
-    "#ifndef GTMI_KBUF_HELPERS",
-    "#define GTMI_KBUF_HELPERS",
-    "namespace gtmi {",
-    "// a whole field as one buffer: offsets past either end (speculative levels) read 0, stores drop",
-    "GTMI_DEV __amdgpu_buffer_rsrc_t field_rsrc(const void* base, int32_t nbytes) {",
-    "    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);",
-    "}",
-    "template <typename T, bool NT> GTMI_DEV T kload(__amdgpu_buffer_rsrc_t rs, int32_t off) {",
-    "    T v;",
-    "    if constexpr (sizeof(T) == 8) { const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 8); }",
-    "    else if constexpr (sizeof(T) == 4) { const auto x = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 4); }",
-    "    else if constexpr (sizeof(T) == 2) { const auto x = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 2); }",
-    "    else { const auto x = __builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, NT ? 2 : 0); __builtin_memcpy(&v, &x, 1); }",
-    "    return v;",
-    "}",
-    "template <typename T, bool NT> GTMI_DEV void kstore(__amdgpu_buffer_rsrc_t rs, int32_t off, T v) {",
-    "    if constexpr (sizeof(T) == 8) { decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 8); __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, NT ? 2 : 0); }",
-    "    else if constexpr (sizeof(T) == 4) { decltype(__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 4); __builtin_amdgcn_raw_buffer_store_b32(x, rs, off, 0, NT ? 2 : 0); }",
-    "    else if constexpr (sizeof(T) == 2) { decltype(__builtin_amdgcn_raw_buffer_load_b16(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 2); __builtin_amdgcn_raw_buffer_store_b16(x, rs, off, 0, NT ? 2 : 0); }",
-    "    else { decltype(__builtin_amdgcn_raw_buffer_load_b8(rs, 0, 0, 0)) x; __builtin_memcpy(&x, &v, 1); __builtin_amdgcn_raw_buffer_store_b8(x, rs, off, 0, NT ? 2 : 0); }",
-    "}",
-    "// KB: the buffer form; else the clamped 64-bit address of the same level",
-    "template <bool KB, typename T, bool NT> GTMI_DEV T kld(__amdgpu_buffer_rsrc_t rs, int32_t lo, int32_t kb, const T* cb,",
-    "                                                     int kk, int klo, int khi, int64_t sK) {",
-    "    if constexpr (KB) return kload<T, NT>(rs, lo + kk * kb);",
-    "    else return sload<T, NT>(cb + (int64_t)clampi(kk, klo, khi) * sK);",
-    "}",
-    "template <bool KB, typename T, bool NT> GTMI_DEV void kst(__amdgpu_buffer_rsrc_t rs, int32_t lo, int32_t kb, T* cb,",
-    "                                                        int kk, int klo, int khi, int64_t sK, T v) {",
-    "    if constexpr (KB) kstore<T, NT>(rs, lo + kk * kb, v);",
-    "    else sstore<T, NT>(cb + (int64_t)clampi(kk, klo, khi) * sK, v);",
-    "}",
-    "}  // namespace gtmi",
-    "#endif",
-    "",
-]
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -135,9 +95,6 @@ class ColumnGen:
         self.ext = (ilo, ihi, jlo, jhi)
         self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
         self.tile = bool(getattr(kernel, "tile", False))
-        # K-streaming loads/stores through field-wide buffer descriptors (option ``kbuf``): one
-        # 32-bit offset per access instead of a clamped 64-bit address, out-of-range levels read 0
-        self.kbuf = int(opts.get("kbuf", DEFAULT_KBUF)) == 1 and not self.tile
         self.lds = set(getattr(kernel, "lds", ()))
         if self.tile:
             bx, by = self._block()
@@ -423,12 +380,10 @@ class ColumnGen:
                 if self._mem(n) and n not in self.scratch and not (read_loops.get(n, set()) - wl)
             }
         scalars = st.scalar_params()
-        L = list(KBUF_HELPERS) if self.kbuf else []
+        L = []
         L.append(f"struct K{k}Params {{")
         for s in used:
             L += ["    " + x for x in kparam_decl(s, s.name in written)]
-            if self.kbuf:
-                L.append(f"    const void* b_{s.c}; int32_t nb_{s.c};  // the whole field as one buffer (KB)")
         for s in scalars:
             L.append(f"    {s.dtype.ctype} s_{cname(s.name)};")
         L.append("    int32_t ni, nj, nk;")
@@ -436,8 +391,6 @@ class ColumnGen:
         L.append("};")
         L.append("")
         bx, by = self._block()
-        if self.kbuf:
-            L.append("template <bool KB>")
         L.append(f"__global__ void __launch_bounds__({bx * by}) k{k}_column(const K{k}Params p) {{")
         B = []
         eilo, eihi, ejlo, ejhi = self.ext
@@ -492,14 +445,6 @@ class ColumnGen:
                 for acc, w in iter_accesses(sec.body):
                     if isinstance(acc, ir.FieldAccess) and acc.name in inf.direct:
                         self._base(acc.name, acc.offset[0], acc.offset[1], B, acc.name in written)
-        if self.kbuf:
-            # one descriptor per field (wave-uniform: kernel arguments only), the level stride in
-            # bytes, and each column base as a byte offset into the field's buffer
-            for s in used:
-                B.append(f"const __amdgpu_buffer_rsrc_t rs_{s.c} = gtmi::field_rsrc(p.b_{s.c}, KB ? p.nb_{s.c} : 0);")
-                B.append(f"const int32_t kb_{s.c} = (int32_t)p.sK_{s.c} * (int32_t)sizeof(*p.p_{s.c});")
-            for (name, di, dj), v in list(self.bases.items()):
-                B.append(f"const int32_t lo_{v[3:]} = KB ? (int32_t)((const char*){v} - (const char*)p.b_{cname(name)}) : 0;")
         if self.tail is not None:
             t = self.tail
             B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
@@ -558,9 +503,8 @@ class ColumnGen:
             lds = f"(size_t)p.tail_len * {self.tail_per_level}"
             H.append("        static bool lds_attr = false;")
             H.append("        if (!lds_attr) {")
-            for inst in ((f"k{k}_column<true>", f"k{k}_column<false>") if self.kbuf else (f"k{k}_column",)):
-                H.append(f"            hipFuncSetAttribute((const void*){inst}, hipFuncAttributeMaxDynamicSharedMemorySize, "
-                         f"{LDS_BYTES});")
+            H.append(f"            hipFuncSetAttribute((const void*)k{k}_column, hipFuncAttributeMaxDynamicSharedMemorySize, "
+                     f"{LDS_BYTES});")
             H.append("            lds_attr = true;")
             H.append("        }")
         else:
@@ -574,33 +518,7 @@ class ColumnGen:
         else:
             grid = (f"dim3((unsigned)((ni + {eilo + eihi + bx - 1}) / {bx}), "
                     f"(unsigned)((nj + {ejlo + ejhi + by - 1}) / {by})), dim3({bx}, {by}), {lds}, stream, p")
-            if self.kbuf:
-                # KB when every field's bytes, plus the speculative levels the rings and band
-                # prefetches reach past either end, fit a signed 32-bit offset
-                # (the ring reaches kring levels past a section's end; the register band's
-                # prefetches stay inside [0, nk); window offsets add their own reach)
-                look = self.ring + 2 + max((abs(d) for inf in self.info.values() for rng in inf.win.values()
-                                            for d in rng), default=0)
-                H.append("        bool kb_ok = true;")
-                # timing probe only (option ``kbuf_null``: comma-separated fields or "*"): those
-                # fields' descriptors get zero records, so the same instruction stream runs without
-                # their memory traffic (cdna_hip_programming.md, "price ONE buffer's traffic")
-                nl = str(self.opts.get("kbuf_null", ""))
-                null = {s_.name for s_ in used} if nl == "*" else set(filter(None, nl.split(":")))
-                for s in used:
-                    q = f"f[{s.index}]"
-                    H.append(f"        {{  int64_t span = 1; for (int d = 0; d < 3; ++d) span += ({q}.shape[d] - 1) * {q}.strides[d];")
-                    H.append(f"           for (int d = 0; d < {q}.n_data_dims; ++d) span += ({q}.data_shape[d] - 1) * {q}.data_strides[d];")
-                    H.append(f"           const int64_t isz = (int64_t)sizeof(*p.p_{s.c}), nb = span * isz;")
-                    H.append(f"           const int64_t reach = nb + (int64_t){look} * (p.sK_{s.c} < 0 ? -p.sK_{s.c} : p.sK_{s.c}) * isz;")
-                    H.append(f"           bool pos = true; for (int d = 0; d < 3; ++d) pos = pos && {q}.strides[d] >= 0;")
-                    H.append(f"           kb_ok = kb_ok && pos && reach < ((int64_t)1 << 31);")
-                    nb_expr = "0" if str(s.name) in null else f"(int32_t)(nb < ((int64_t)1 << 31) ? nb : 0)"
-                    H.append(f"           p.b_{s.c} = {q}.data; p.nb_{s.c} = {nb_expr}; }}")
-                H.append(f"        if (kb_ok) hipLaunchKernelGGL(k{k}_column<true>, {grid});")
-                H.append(f"        else hipLaunchKernelGGL(k{k}_column<false>, {grid});")
-            else:
-                H.append(f"        hipLaunchKernelGGL(k{k}_column, {grid});")
+            H.append(f"        hipLaunchKernelGGL(k{k}_column, {grid});")
         H.append("    }")
         H.append("}")
         return "\n".join(L), "\n".join(H)
@@ -649,10 +567,6 @@ class ColumnGen:
         def mem_index(name, di, dj, kexpr):
             """A load expression (non-temporal for read-once streams)."""
             nt = "true" if (name in self.nt_loads and name not in direct) else "false"
-            if self.kbuf and name not in direct:
-                c, v = cname(name), self.bases[(name, di, dj)]
-                return (f"gtmi::kld<KB, {decl_dtype[name].ctype}, {nt}>(rs_{c}, lo_{v[3:]}, kb_{c}, {v}, {kexpr}, "
-                        f"p.klo_{c}, p.khi_{c}, p.sK_{c})")
             return f"gtmi::sload<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, di, dj, kexpr)})"
 
         def load_into(var, name, di, dj, kexpr, maybe_cached=True, reg=None) -> List[str]:
@@ -674,12 +588,7 @@ class ColumnGen:
 
         def mem_store(name, kexpr, value):
             nt = "true" if (name in self.nt_stores and name not in direct) else "false"
-            if self.kbuf and name not in direct:
-                c, v = cname(name), self.bases[(name, 0, 0)]
-                st = (f"gtmi::kst<KB, {decl_dtype[name].ctype}, {nt}>(rs_{c}, lo_{v[3:]}, kb_{c}, {v}, {kexpr}, "
-                      f"p.klo_{c}, p.khi_{c}, p.sK_{c}, {value});")
-            else:
-                st = f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
+            st = f"gtmi::sstore<{decl_dtype[name].ctype}, {nt}>({mem_ptr(name, 0, 0, kexpr)}, {value});"
             if name in no_store and kexpr == "k":
                 if band_now[0] == "reg":
                     return "// register band level: kept in registers only"

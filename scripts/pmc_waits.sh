@@ -5,7 +5,7 @@
 #   C  SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE
 # (separate passes; WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES, MI355X_MICROARCH.md
 # "rocprofv3 PMC slots"), then scripts/summarize_waits.py prints the split per config.
-# Usage: CONFIGS="vadv copy" TAG=r05a [BENCH_OPTS="--opt kbuf=1"] bash scripts/pmc_waits.sh
+# Usage: CONFIGS="vadv copy" TAG=r05a [PASSES="A B C D"] [BENCH_OPTS="--opt ..."] bash scripts/pmc_waits.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -15,8 +15,10 @@ mkdir -p $OUT
 PASS_A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES"
 PASS_B="TCC_HIT_sum TCC_MISS_sum"
 PASS_C="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+# D: is an issue stall the memory pipe pushing back? (TA FIFOs full, VMEM instructions in flight)
+PASS_D="SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_WAVE_CYCLES"
 for cfg in ${CONFIGS:-vadv copy}; do
-  for p in A B C; do
+  for p in ${PASSES:-A B C}; do
     eval "ctrs=\$PASS_$p"
     echo "== $cfg pass $p: $ctrs"
     timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/${cfg}_$p -o pmc -- \

@@ -19,7 +19,7 @@ import sys
 
 def counters(out, cfg):
     vals = {}
-    for p in ("A", "B", "C"):
+    for p in ("A", "B", "C", "D"):
         for f in glob.glob(f"{out}/{cfg}_{p}/**/*counter_collection.csv", recursive=True):
             per = {}
             for r in csv.DictReader(open(f)):
@@ -49,6 +49,12 @@ def main():
                 name = f"SQ_ACTIVE_INST_{key}"
                 if name in v and v["SQ_ACTIVE_INST_ANY"]:
                     row[f"issue_share_{key}"] = round(v[name] / v["SQ_ACTIVE_INST_ANY"], 4)
+        if v.get("SQ_INSTS_VMEM") and v.get("SQ_INST_LEVEL_VMEM") is not None:
+            # Little's law: VMEM instructions in flight (summed per cycle) / issued = mean latency
+            row["vmem_latency_quad_cycles"] = round(v["SQ_INST_LEVEL_VMEM"] / v["SQ_INSTS_VMEM"], 1)
+        for f in ("SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL", "SQ_VMEM_WR_TA_DATA_FIFO_FULL"):
+            if f in v and wc:
+                row[f.lower() + "_per_wave_cycle"] = round(v[f] / wc, 5)
         h, m = v.get("TCC_HIT_sum"), v.get("TCC_MISS_sum")
         if h is not None and m is not None and h + m:
             row["L2_hit"] = round(h / (h + m), 4)

@@ -104,8 +104,7 @@ COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tai
                     "tail_fwd_bwd_offsets", "tridiag", "tridiag_k161", "tridiag_k2", "tridiag_k70",
                     "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80",
                     "vertical_advection_dycore_k160", "band_ij_accumulator", "band_ij_accumulator_reader"]
-COLUMN_OPTS = [{"kreg": 96}, {"kreg": 48, "kreg_pf": 6}, {"kreg": 0}, {"ktail_lds": 0}, {"kreg": 40, "kreg_pf": 50},
-               {"kbuf": 1}, {"kbuf": 1, "kreg": 0, "ktail_lds": 0}]
+COLUMN_OPTS = [{"kreg": 96}, {"kreg": 48, "kreg_pf": 6}, {"kreg": 0}, {"ktail_lds": 0}, {"kreg": 40, "kreg_pf": 50}]
 
 
 @pytest.mark.parametrize("opts", COLUMN_OPTS, ids=lambda o: "_".join(f"{k}{v}" for k, v in o.items()))
