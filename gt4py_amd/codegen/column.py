@@ -48,6 +48,7 @@ AUTO_KREG_API_PF = 6
 # round 5: the per-section prefetch, deeper prefetch for light loops (kpf_adapt),
 # I-neighbour lane shifts (nbr_shfl) and split cached/uncached writer segments (seg_tail).
 BAND_PF_OVER_RING = 2
+DEFAULT_TAIL_HEAD = -1  # auto: see ColumnGen._plan_tail
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
 
 
@@ -68,6 +69,14 @@ class _Tail:
     a_fwd: bool
     fields: List[str]
     no_store: Set[str]  # scratch fields whose cached levels are never written to memory
+    # head: the FIRST levels of loop a's sweep stay on chip (the reader re-reads the last ones,
+    # written just before the turn, from the Infinity Cache); else the LAST ones (tail)
+    head: bool = False
+
+    @property
+    def low(self) -> bool:
+        """The cached levels are the lowest ones, [0, kreg + L) (else the highest)."""
+        return self.a_fwd == self.head
 
     def var(self, name):
         return f"tl_{cname(name)}"
@@ -269,6 +278,17 @@ class ColumnGen:
                 best = _Tail(la, lb, A.fwd, fields, no_store)
         if best is None:
             return None
+        # which end of the writer's sweep stays on chip (option ``ktail_head``: 1 head, 0 tail,
+        # -1 auto): a re-read level costs HBM bytes unless it was written recently enough to be
+        # in the 256-MB Infinity Cache, i.e. unless it is one of the writer's LAST levels -- so
+        # cached API outputs (re-read, never skipped) keep the FIRST levels on chip (lab:
+        # scripts/lab/headtail_lab.hip, tridiag with 40 LDS levels 2.245 -> 2.152 ms). Write-free
+        # scratch tails keep the last levels: their big register band would stay live through
+        # both memory sweeps.
+        head = int(self.opts.get("ktail_head", DEFAULT_TAIL_HEAD))
+        if head < 0:
+            head = 1 if not all(n in best.no_store for n in best.fields) else 0
+        best.head = bool(head)
         per_level = 256 * sum(self.st.decl(n).dtype.itemsize for n in best.fields)
         self.tail_lmax = budget // per_level
         if self.tail_lmax < 1:
@@ -317,7 +337,7 @@ class ColumnGen:
             secs = self.st.vertical_loops[li].sections
             m = []
             for u in range(R):
-                lev = (ir.LevelMarker.END, u - R) if t.a_fwd else (ir.LevelMarker.START, u)
+                lev = (ir.LevelMarker.START, u) if t.low else (ir.LevelMarker.END, u - R)
                 hit = [si for si, sec in enumerate(secs)
                        if _ge(lev, sec.interval.start) and not _ge(lev, sec.interval.end)]
                 m.append(hit[0] if hit else None)
@@ -459,7 +479,7 @@ class ColumnGen:
             else:
                 B.append("const int rbase = 0;")
             B.append("const int tlen = p.tail_len < nk - rbase ? p.tail_len : nk - rbase;")
-            if t.a_fwd:
+            if not t.low:
                 B.append("const int tc1 = nk - rbase, tc0 = tc1 - tlen;  // LDS-cached levels [tc0, tc1)")
             else:
                 B.append("const int tc0 = rbase, tc1 = rbase + tlen;  // LDS-cached levels [tc0, tc1)")
@@ -472,7 +492,7 @@ class ColumnGen:
         # reader is rendered first so that the writer's last band levels can issue the reader's
         # first band prefetches (declared here, at kernel scope)
         t_ = self.tail
-        self._xpf = bool(self.kreg) and t_ is not None \
+        self._xpf = bool(self.kreg) and t_ is not None and not t_.head \
             and t_.a != t_.b and t_.b in self.kernel.loops and t_.a in self.kernel.loops \
             and self.kernel.loops.index(t_.b) == self.kernel.loops.index(t_.a) + 1
         if self._xpf:
@@ -654,7 +674,7 @@ class ColumnGen:
         # at a section boundary
         if R:
             Pb = int(self.opts.get("kreg_pf", self.band_pf_default if self.band_pf_default is not None else P + BAND_PF_OVER_RING))
-            kexpr_of = (lambda u_: f"nk - {R} + {u_}") if tail.a_fwd else (lambda u_: f"{u_}")  # noqa: E731
+            kexpr_of = (lambda u_: f"{u_}") if tail.low else (lambda u_: f"nk - {R} + {u_}")  # noqa: E731
             all_us = sorted((u for u in range(R) if band_map[u] is not None), reverse=not fwd)
             mem_keys = {}
             for u in all_us:
@@ -718,7 +738,7 @@ class ColumnGen:
             out.append(f"        int ks = {lo}, ke = {hi};")
             out.append("        if (ks < 0) ks = 0; if (ke > nk) ke = nk;")
             if R:  # the register band's levels run in the unrolled band code
-                out.append("        if (ke > nk - rbase) ke = nk - rbase;" if tail.a_fwd else "        if (ks < rbase) ks = rbase;")
+                out.append("        if (ks < rbase) ks = rbase;" if tail.low else "        if (ke > nk - rbase) ke = nk - rbase;")
 
             def kaddr(acc: ir.FieldAccess) -> str:
                 kexpr = f"k + ({acc.offset[2]})"
@@ -917,7 +937,17 @@ class ColumnGen:
                 out.append(f"        const int x3 = {mx('x2', f'tc1 - ({hi_fd})')}, x4 = tc1 - ({lo_fd});  // x1 <= x2 <= x3 <= x4")
                 x1, x2, x3, x4 = "x1", "x2", "x3", "x4"
                 rng_ = lambda a, b: (mx("ks", a) if a else "ks", mn("ke", b) if b else "ke")  # noqa: E731
-                if fwd:
+                if tail.head:
+                    # the cache sits at the END of this (reading) sweep: stream the levels before
+                    # it with the ring, each side of it the levels whose fronts straddle its edge
+                    out.append("        const int x4b = x4 > x3 ? x4 : x3;")
+                    if fwd:
+                        parts = [(*rng_(None, x1), "mem"), (*rng_(x1, x2), "mixed"), (*rng_(x2, x3), "lds"),
+                                 (*rng_(x3, "x4b"), "mixed"), (*rng_("x4b", None), "mem")]
+                    else:
+                        parts = [(*rng_("x4b", None), "mem"), (*rng_(x3, "x4b"), "mixed"), (*rng_(x2, x3), "lds"),
+                                 (*rng_(x1, x2), "mixed"), (*rng_(None, x1), "mem")]
+                elif fwd:
                     parts = [(*rng_(None, x2), "mixed"), (*rng_(x2, x3), "lds"), (*rng_(x3, x4), "mixed"),
                              (*rng_(x4, None), "mem")]
                 else:
@@ -964,10 +994,10 @@ class ColumnGen:
                 bc.append("    }")
                 band_code += bc
         if band_code:
-            if li == tail.a:
-                out += band_code  # the band ends the writer's sweep
+            if (li == tail.a) != tail.head:
+                out += band_code  # the band ends the writer's sweep (tail) or the reader's (head)
             else:
-                out[sec_start:sec_start] = band_code  # and starts the reader's
+                out[sec_start:sec_start] = band_code  # and starts the other one
         out.append("}")
         return out
 

@@ -98,13 +98,15 @@ def test_golden_case(name):
 
 
 # column-kernel schedules: the two register bands the auto rule (kreg=-1) selects, forced onto every
-# case (96 levels, prefetch ring + 2; 48 levels, prefetch 6), no register band, no LDS tail, and a
-# prefetch distance longer than the band (the writer's prologue carries the reader's first levels)
+# case (96 levels, prefetch ring + 2; 48 levels, prefetch 6), no register band, no LDS tail, a
+# prefetch distance longer than the band (the writer's prologue carries the reader's first levels),
+# and both ends of the writer's sweep on chip (ktail_head), with and without a register band
 COLUMN_OPT_CASES = ["kcache_forward_backward", "section_gap_register_temp", "tail_bwd_fwd", "tail_bwd_fwd_short",
                     "tail_fwd_bwd_offsets", "tridiag", "tridiag_k161", "tridiag_k2", "tridiag_k70",
                     "tridiag_subdomain_k70", "vertical_advection_dycore", "vertical_advection_dycore_k80",
                     "vertical_advection_dycore_k160", "band_ij_accumulator", "band_ij_accumulator_reader"]
-COLUMN_OPTS = [{"kreg": 96}, {"kreg": 48, "kreg_pf": 6}, {"kreg": 0}, {"ktail_lds": 0}, {"kreg": 40, "kreg_pf": 50}]
+COLUMN_OPTS = [{"kreg": 96}, {"kreg": 48, "kreg_pf": 6}, {"kreg": 0}, {"ktail_lds": 0}, {"kreg": 40, "kreg_pf": 50},
+               {"ktail_head": 1}, {"ktail_head": 0}, {"ktail_head": 1, "kreg": 0}, {"ktail_head": 1, "kreg": 40, "kreg_pf": 50}]
 
 
 @pytest.mark.parametrize("opts", COLUMN_OPTS, ids=lambda o: "_".join(f"{k}{v}" for k, v in o.items()))
