@@ -142,3 +142,23 @@ def test_register_band_never_prefetches_written_ij_fields(name, opts):
     prefetched = set(re.findall(r"\bbp\d+_w(\d+)_(\w+?)_p0_p0_", src))
     assert ("1", "s") not in prefetched and ("0", "lev") not in prefetched, prefetched
     assert {n for _, n in prefetched} >= {"a", "b"}
+
+
+def test_sweep_cache_end_auto_rule():
+    """ktail_head auto: cached API outputs (tridiag's sup/rhs, re-read anyway) keep the FIRST
+    forward levels on chip, so the re-read ones come from the Infinity Cache; write-free scratch
+    (vadv's ccol/dcol, whose 96-level register band would stay live through both memory sweeps)
+    keeps the last ones. The writer's LDS band then sits at [rbase, rbase + tlen) or just below
+    nk - rbase."""
+    import bench
+
+    srcs = {}
+    for cfg in ("tridiag", "vadv"):
+        sname, dtype, *_ = bench.CONFIGS[cfg]
+        st = gtscript.stencil(backend="gt:mi355x", definition=bench.stencil_defs()[(sname, dtype)],
+                              name=f"bench.{cfg}", device_sync=False, externals=bench.EXTERNALS.get(sname, {}))
+        srcs[cfg] = st._gt_run_impl_.compiled.source
+    assert "const int tc0 = rbase, tc1 = rbase + tlen;" in srcs["tridiag"]
+    assert "if (ks < rbase) ks = rbase;" in srcs["tridiag"]
+    assert "const int tc1 = nk - rbase, tc0 = tc1 - tlen;" in srcs["vadv"]
+    assert "the reader's band: prefetched here" in srcs["vadv"] and "the reader's band" not in srcs["tridiag"]
