@@ -125,7 +125,6 @@ class Mi355xBackend(BaseBackend):
         "bufld": {"versioning": True, "type": int, "description": "plane kernels: interior strips load rows through buffer descriptors, branch-free, so prefetched rows stay in flight (1 on, 0 off, -1 auto: on for 4-cell lanes, default)"},
         "tile": {"versioning": True, "type": int, "description": "sequential sweeps that read their own products across columns: tile kernels with LDS planes (1, default) instead of the staged lowering (0)"},
         "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per block (4, 8, 16)"},
-        "tile_rows": {"versioning": True, "type": int, "description": "tile kernels: J rows per thread (1, or 2: the block covers twice tile_by rows, each thread two columns)"},
         "tile_bx": {"versioning": True, "type": int, "description": "tile kernels: I lanes per block (64 or 128)"},
         "tile_ti": {"versioning": True, "type": int, "description": "tile kernels: output columns per tile in I (default: 64 minus the sweep's I extent)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},

@@ -25,7 +25,6 @@ vertical loop of the kernel in loop order. See ``codegen/hip.py`` and DESIGN.md 
 from __future__ import annotations
 
 import dataclasses
-import re
 from typing import Dict, List, Optional, Set, Tuple
 
 from gt4py_amd import ir
@@ -51,14 +50,6 @@ AUTO_KREG_API_PF = 6
 BAND_PF_OVER_RING = 2
 DEFAULT_TAIL_HEAD = -1  # auto: see ColumnGen._plan_tail
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
-TILE_ROWS = 1  # tile mode: J rows per thread (2: the block covers 2 x tile_by rows, register-blocked)
-_ROW1 = re.compile(r"\b(w\d+_\w+|rg\d+_\w+|cb_\w+|j|ty|alive|own)\b")
-
-
-def _row1(line: str) -> str:
-    """Tile mode, second row of a thread: the same code on its own column state (window and ring
-    registers, column bases, j, ty, alive, own renamed)."""
-    return _ROW1.sub(r"\1_r1", line)
 
 
 @dataclasses.dataclass
@@ -114,12 +105,8 @@ class ColumnGen:
         self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
         self.tile = bool(getattr(kernel, "tile", False))
         self.lds = set(getattr(kernel, "lds", ()))
-        self.trows = int(opts.get("tile_rows", TILE_ROWS)) if self.tile else 1
-        if self.trows not in (1, 2):
-            raise ValueError(f"tile_rows must be 1 or 2, got {self.trows}")
         if self.tile:
             bx, by = self._block()
-            by *= self.trows
             if bx - ilo - ihi < 8 or by - jlo - jhi < 1:
                 raise UnsupportedStencil(f"IJ extent {self.ext} too wide for a {bx}x{by} tile")
             ti = int(opts.get("tile_ti", 0))
@@ -165,7 +152,7 @@ class ColumnGen:
             unit = (128 if item >= 8 else 64) // item
             if ti >= unit:
                 ti -= ti % unit
-        return ti, by * self.trows - ejlo - ejhi
+        return ti, by - ejlo - ejhi
 
     def _tile_item(self) -> int:
         """Largest cell size among the API fields the tile kernel stores (8 if none)."""
@@ -445,14 +432,9 @@ class ColumnGen:
             B.append(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};")
             B.append(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && ty < {ejlo + TJ} && "
                      f"i < p.ni && j < p.nj;")
-            if self.trows == 2:  # the thread's second row, by rows further down the tile
-                B.append(f"const int ty_r1 = ty + {by}, j_r1 = j + {by};")
-                B.append(_row1(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};"))
-                B.append(_row1(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && ty < {ejlo + TJ} && "
-                               f"i < p.ni && j < p.nj;"))
             for n in sorted(self.lds):
                 ct = self.st.decl(n).dtype.ctype
-                B.append(f"__shared__ {ct} lds_{cname(n)}[2][{by * self.trows}][{bx}];  // this level's plane (k & 1)")
+                B.append(f"__shared__ {ct} lds_{cname(n)}[2][{by}][{bx}];  // this level's plane (k & 1)")
         elif int(self.opts.get("col_order", 1)) == 1:
             # XCD-aware: consecutive column blocks (along I, then J) run on one XCD (8 XCDs, round-robin dispatch)
             B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
@@ -471,7 +453,6 @@ class ColumnGen:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
         # column base pointers: the i/j part of every address, computed once per thread
         self.bases: Dict[Tuple[str, int, int], str] = {}
-        nb0 = len(B)
         for li in self.kernel.loops:
             inf = self.info[li]
             for (name, di, dj) in list(inf.win) + [(n, None, None) for n in sorted(inf.direct)]:
@@ -484,8 +465,6 @@ class ColumnGen:
                 for acc, w in iter_accesses(sec.body):
                     if isinstance(acc, ir.FieldAccess) and acc.name in inf.direct:
                         self._base(acc.name, acc.offset[0], acc.offset[1], B, acc.name in written)
-        if self.trows == 2:
-            B += [_row1(x) for x in B[nb0:]]
         if self.tail is not None:
             t = self.tail
             B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
@@ -641,34 +620,11 @@ class ColumnGen:
 
         P = self.ring
         step = "+" if fwd else "-"
-        def dup(code: List[str]) -> List[str]:
-            """Per-column code for every row of the thread (tile_rows)."""
-            return code + [_row1(x) for x in code] if self.trows == 2 else code
-
-        def merged(stmts: List[str]) -> List[str]:
-            """A level's statements for every row of the thread, interleaved between the LDS
-            barriers (both rows' planes are written before any row reads across columns)."""
-            if self.trows == 1:
-                return stmts
-            chunks, cur = [], []
-            for x in stmts[1:]:  # stmts[0]: k_next (one per level)
-                if x.startswith("gtmi::lds_barrier();"):
-                    chunks.append((cur, x))
-                    cur = []
-                else:
-                    cur.append(x)
-            res = stmts[:1]
-            for c, bar in chunks:
-                res += c + [_row1(x) for x in c] + [bar]
-            return res + cur + [_row1(x) for x in cur]
-
         out = [f"{{  // vertical loop {li} ({order.name})"]
-        decls = []
         for (name, di, dj), rng in win.items():
             t = decl_dtype[name].ctype
             for d in range(rng[0], rng[1] + 1):
-                decls.append(f"    {t} {wvar(name, di, dj, d)} = ({t})0;")
-        out += dup(decls)
+                out.append(f"    {t} {wvar(name, di, dj, d)} = ({t})0;")
         out.append("    int k_next = -0x7fffffff;")
         front = {}
         for key, rng in win.items():
@@ -889,9 +845,9 @@ class ColumnGen:
             def entry_level(slot, mode) -> List[str]:
                 """A segment's first level, which may follow a gap: full window reload unless it
                 continues the sweep (the only level with loads inside a branch)."""
-                return (["if (k != k_next) {  // (re)load the full K-window"] + ["    " + x for x in dup(reload())]
-                        + ["} else {"] + ["    " + x for x in dup(shift_and_fronts(slot, mode))] + ["}"]
-                        + merged(statements()))
+                return (["if (k != k_next) {  // (re)load the full K-window"] + ["    " + x for x in reload()]
+                        + ["} else {"] + ["    " + x for x in shift_and_fronts(slot, mode)] + ["}"]
+                        + statements())
 
             def refill(slot, R, keys) -> List[str]:
                 body = []
@@ -920,24 +876,23 @@ class ColumnGen:
                         o.append("        for (int k = ss + 1; k < se; ++k) {")
                     else:
                         o.append("        for (int k = se - 2; k >= ss; --k) {")
-                    o += ["            " + x for x in dup(shift_and_fronts(None, mode)) + merged(statements())]
+                    o += ["            " + x for x in shift_and_fronts(None, mode) + statements()]
                     o.append("        }")
                     o.append("    }")
                     o.append("}")
                     return o
-                pro = []
                 for u in range(R):
                     for key in keys:
                         fv = wvar(*key, front[key])
                         t = decl_dtype[key[0]].ctype
-                        pro.append(f"{t} rg{u}_{fv};")
-                        pro += load_into(f"rg{u}_{fv}", *key, f"{first} {step} {u} + ({front[key]})", maybe_cached=False)
-                o += ["        " + x for x in dup(pro)]
+                        o.append(f"        {t} rg{u}_{fv};")
+                        o += ["        " + x for x in load_into(f"rg{u}_{fv}", *key, f"{first} {step} {u} + ({front[key]})",
+                                                                maybe_cached=False)]
                 # first level: reload or continue; ring slot 0
                 o.append("        {")
                 o.append(f"            const int k = {first};")
                 o += ["            " + x for x in entry_level(0, mode)]
-                o += ["            " + x for x in dup(refill(0, R, keys))]
+                o += ["            " + x for x in refill(0, R, keys)]
                 o.append("        }")
                 # full blocks of R levels: shift only, no branches around loads (a load inside a
                 # branch makes the compiler drain every load in flight at the join)
@@ -951,8 +906,8 @@ class ColumnGen:
                     slot = (u + 1) % R
                     o.append(f"            {{  // ring slot {slot}")
                     o.append(f"                const int k = kb {step} {u};")
-                    o += ["                " + x for x in dup(shift_and_fronts(slot, mode)) + merged(statements())
-                          + dup(refill(slot, R, keys))]
+                    o += ["                " + x for x in shift_and_fronts(slot, mode) + statements()
+                          + refill(slot, R, keys)]
                     o.append("            }")
                 o.append("        }")
                 # the last < R levels: their fronts are already in the ring
@@ -961,7 +916,7 @@ class ColumnGen:
                     cond = f"kb + {u} < se" if fwd else f"kb - {u} >= ss"
                     o.append(f"        if ({cond}) {{  // ring slot {slot}")
                     o.append(f"            const int k = kb {step} {u};")
-                    o += ["            " + x for x in dup(shift_and_fronts(slot, mode)) + merged(statements())]
+                    o += ["            " + x for x in shift_and_fronts(slot, mode) + statements()]
                     o.append("        }")
                 o.append("    }")
                 o.append("}")
