@@ -118,3 +118,25 @@ def test_bench_gpu_line_with_placement_tuning():
     assert rec["full_call"]["overhead_vs"] == "kernel_ms"
     r = rec["roofline"]
     assert 0.0 < r["frac_untuned"] <= 1.0 and r["kernel_ms_untuned"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_halo_selfcomm_link_probe():
+    """One GPU as its own periodic neighbour through RCCL (``--halo-selfcomm``): the line carries
+    the link probe of the one rank (peer = itself, payload intact) next to the halo A/B."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    res = _run(["--config", "lap5", "--steps", "3", "--warmup", "1", "--no-extra", "--no-cpu-baseline", "--sustain", "0",
+                "--placement-candidates", "0", "--halo-selfcomm"],
+               env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                          "MASTER_PORT": str(port)}, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    rec = json.loads([ln for ln in res.stdout.splitlines() if ln.strip()][-1])
+    lp = rec["dist"]["link_probe"]
+    (r0,) = lp["ranks"]
+    assert r0["peers"] == [0] and r0["payload_ok"] and r0["GBps_per_link_each_way"] > 0
+    assert rec["halo_ab"]["overhead"] > -0.5
