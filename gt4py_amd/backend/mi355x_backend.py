@@ -118,6 +118,7 @@ class Mi355xBackend(BaseBackend):
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "kreg_pf": {"versioning": True, "type": int, "description": "column kernels: register-band levels whose memory fronts are loaded ahead (default: the load ring depth + 2; 0 = at their level)"},
         "ktail_head": {"versioning": True, "type": int, "description": "column kernels: keep the FIRST levels of the writer's sweep on chip (1), the last (0), or auto (-1: first for cached API outputs, last for write-free scratch)"},
+        "probe_nobar": {"versioning": True, "type": int, "description": "PROBE"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},
@@ -125,6 +126,7 @@ class Mi355xBackend(BaseBackend):
         "bufld": {"versioning": True, "type": int, "description": "plane kernels: interior strips load rows through buffer descriptors, branch-free, so prefetched rows stay in flight (1 on, 0 off, -1 auto: on for 4-cell lanes, default)"},
         "tile": {"versioning": True, "type": int, "description": "sequential sweeps that read their own products across columns: tile kernels with LDS planes (1, default) instead of the staged lowering (0)"},
         "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per block (4, 8, 16)"},
+        "tile_lblock": {"versioning": True, "type": int, "description": "tile kernels: levels per LDS barrier in the steady-state loop (1, 2, 4)"},
         "tile_bx": {"versioning": True, "type": int, "description": "tile kernels: I lanes per block (64 or 128)"},
         "tile_ti": {"versioning": True, "type": int, "description": "tile kernels: output columns per tile in I (default: 64 minus the sweep's I extent)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},

@@ -25,6 +25,7 @@ vertical loop of the kernel in loop order. See ``codegen/hip.py`` and DESIGN.md 
 from __future__ import annotations
 
 import dataclasses
+import re
 from typing import Dict, List, Optional, Set, Tuple
 
 from gt4py_amd import ir
@@ -50,6 +51,15 @@ AUTO_KREG_API_PF = 6
 BAND_PF_OVER_RING = 2
 DEFAULT_TAIL_HEAD = -1  # auto: see ColumnGen._plan_tail
 TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
+# tile mode: levels per LDS barrier in the steady-state loop (a level's statements after the barrier
+# wait for the next level's before it; planes rotate over 2 x TILE_LBLOCK buffers). Every tile
+# program at 1024^2x80 (profiles/r05/r05l_tile_probe.log): tile_f32 -6 %, bwd_recurrence -1.8 %,
+# scratch_product -0.8 %, staged -0.6 %, the rest within +-0.4 %; kernels where no loop can be
+# blocked keep two planes and one barrier per level.
+TILE_LBLOCK = 2
+_KVAR = re.compile(r"\bk\b")
+_WVAR = re.compile(r"\bw\d+_\w+")
+_WASSIGN = re.compile(r"^\s*(w\d+_\w+) = ")
 
 
 @dataclasses.dataclass
@@ -105,6 +115,12 @@ class ColumnGen:
         self.ring = max(0, int(opts.get("kring", DEFAULT_RING)))
         self.tile = bool(getattr(kernel, "tile", False))
         self.lds = set(getattr(kernel, "lds", ()))
+        # tile mode: levels per LDS barrier in the steady-state loop (option ``tile_lblock``); the
+        # planes rotate over 2 x that many buffers
+        self.lblock = int(opts.get("tile_lblock", TILE_LBLOCK)) if self.tile else 1
+        if self.lblock not in (1, 2, 4):
+            raise ValueError(f"tile_lblock must be 1, 2 or 4, got {self.lblock}")
+        self.pmask = "1" if self.lblock == 1 else str(2 * self.lblock - 1)
         if self.tile:
             bx, by = self._block()
             if bx - ilo - ihi < 8 or by - jlo - jhi < 1:
@@ -434,7 +450,7 @@ class ColumnGen:
                      f"i < p.ni && j < p.nj;")
             for n in sorted(self.lds):
                 ct = self.st.decl(n).dtype.ctype
-                B.append(f"__shared__ {ct} lds_{cname(n)}[2][{by}][{bx}];  // this level's plane (k & 1)")
+                B.append(f"__shared__ {ct} lds_{cname(n)}[{2 * self.lblock}][{by}][{bx}];  // this level's plane (k & {self.pmask})")
         elif int(self.opts.get("col_order", 1)) == 1:
             # XCD-aware: consecutive column blocks (along I, then J) run on one XCD (8 XCDs, round-robin dispatch)
             B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
@@ -503,7 +519,12 @@ class ColumnGen:
             self._xpf = not (clash - set(t_.fields))
         self._xpf_decls, self._xpf_loads = [], []
         order = [t_.b] + [x for x in self.kernel.loops if x != t_.b] if self._xpf else list(self.kernel.loops)
+        self._blocked_any = False
         rendered = {li: self._render_loop(li) for li in order}
+        if self.lblock > 1 and not self._blocked_any:
+            # nothing could be blocked: two planes, as with tile_lblock=1
+            self.lblock, self.pmask = 1, "1"
+            return self.render()
         B += self._xpf_decls
         for li in self.kernel.loops:
             B += rendered[li]
@@ -542,6 +563,22 @@ class ColumnGen:
         H.append("    }")
         H.append("}")
         return "\n".join(L), "\n".join(H)
+
+    @staticmethod
+    def _blockable(levels: List[List[str]], shift: List[str]) -> bool:
+        """Can a level's statements after its LDS barrier wait until the next level's statements
+        before it have run? Exactly one barrier per level, no plane written after it, and no
+        window value assigned after it that the next level's shift or statements read."""
+        st = levels[0]
+        bars = [q for q, x in enumerate(st) if x.startswith("gtmi::lds_barrier();")]
+        if len(bars) != 1:
+            return False
+        post = st[bars[0] + 1:]
+        if any("lds_" in x and "] = " in x for x in post):
+            return False
+        assigned = {m.group(1) for x in post for m in [_WASSIGN.match(x)] if m}
+        later = "\n".join(shift + levels[1][:bars[0]])
+        return not any(re.search(r"\b" + re.escape(n) + r"\b", later) for n in assigned)
 
     def _base(self, name, di, dj, out: List[str], writable: bool) -> str:
         key = (name, di, dj)
@@ -751,7 +788,7 @@ class ColumnGen:
                 if acc.name in direct:
                     return mem_index(acc.name, di, dj, kaddr(acc))
                 if acc.name in self.lds and (di or dj):
-                    return f"lds_{cname(acc.name)}[k & 1][ty + ({dj})][tx + ({di})]"
+                    return f"lds_{cname(acc.name)}[k & {self.pmask}][ty + ({dj})][tx + ({di})]"
                 return wvar(acc.name, di, dj, dk)
 
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
@@ -812,7 +849,7 @@ class ColumnGen:
                                  if not w and isinstance(a, ir.FieldAccess) and a.name in self.lds
                                  and (a.offset[0] or a.offset[1])}
                         if reads & pending:
-                            body.append("gtmi::lds_barrier();  // the level's planes are complete")
+                            body.append("gtmi::lds_barrier();  // the level's planes are complete" if not self.opts.get("probe_nobar") else "// probe: no barrier")
                             pending.clear()
                     code = self._stmt(s, rend, wvar, mem_store)
                     g = self._guard(li, si, ti)
@@ -827,7 +864,7 @@ class ColumnGen:
                 if pending:
                     # planes written but not read across columns at this level: the next write of
                     # the same buffer (two levels on) must not overtake a slow reader
-                    body.append("gtmi::lds_barrier();")
+                    body.append("gtmi::lds_barrier();" if not self.opts.get("probe_nobar") else "// probe: no barrier")
                 if tail_write and band_now[0] == "reg":
                     body.append("// register band: this level's final values")
                     body += [f"rb_{cname(n)}_{reg_now[0]} = {wvar(n, 0, 0, 0)};" for n in tail_write]
@@ -902,12 +939,39 @@ class ColumnGen:
                 else:
                     o.append("        int kb = se - 2;")
                     o.append(f"        for (; kb - {R - 1} >= ss; kb -= {R}) {{")
-                for u in range(R):
-                    slot = (u + 1) % R
-                    o.append(f"            {{  // ring slot {slot}")
-                    o.append(f"                const int k = kb {step} {u};")
-                    o += ["                " + x for x in shift_and_fronts(slot, mode) + statements()
-                          + refill(slot, R, keys)]
+                blocked = self.lblock > 1 and R % self.lblock == 0 and \
+                    self._blockable([statements() for _ in range(2)], shift_and_fronts(1 % R, mode))
+                self._blocked_any |= blocked
+                for g in range(0, R, self.lblock if blocked else 1):
+                    if not blocked:
+                        u, slot = g, (g + 1) % R
+                        o.append(f"            {{  // ring slot {slot}")
+                        o.append(f"                const int k = kb {step} {u};")
+                        o += ["                " + x for x in shift_and_fronts(slot, mode) + statements()
+                              + refill(slot, R, keys)]
+                        o.append("            }")
+                        continue
+                    # tile mode, several levels per LDS barrier: every level's statements before
+                    # the barrier (the plane writes), one barrier, then every level's statements
+                    # after it on snapshots of the window values they read
+                    o.append(f"            {{  // levels kb {step} {g} .. {g + self.lblock - 1}: one LDS barrier")
+                    posts = []
+                    for b in range(self.lblock):
+                        u, slot = g + b, (g + b + 1) % R
+                        kv = f"k{b}_"
+                        ren = lambda x, kv=kv: _KVAR.sub(kv, x)  # noqa: E731
+                        o.append(f"                const int {kv} = kb {step} {u};")
+                        st = statements()
+                        cut = next(q for q, x in enumerate(st) if x.startswith("gtmi::lds_barrier();"))
+                        pre, post = st[:cut], st[cut + 1:]
+                        names = sorted(set(_WVAR.findall("\n".join(post))))
+                        o += ["                " + ren(x) for x in shift_and_fronts(slot, mode) + pre]
+                        o += [f"                auto sn{b}_{n} = {n};" for n in names]
+                        o += ["                " + ren(x) for x in refill(slot, R, keys)]
+                        snap = re.compile(r"\b(" + "|".join(map(re.escape, names)) + r")\b") if names else None
+                        posts += [ren(snap.sub(lambda m, b=b: f"sn{b}_{m.group(1)}", x) if snap else x) for x in post]
+                    o.append("                gtmi::lds_barrier();  // the block's planes are complete")
+                    o += ["                " + x for x in posts]
                     o.append("            }")
                 o.append("        }")
                 # the last < R levels: their fronts are already in the ring
@@ -1014,7 +1078,7 @@ class ColumnGen:
             tgt = wvar(name, 0, 0, 0)
             out = [f"{tgt} = {rend(s.value)};"]
             if name in self.lds:
-                out.append(f"lds_{cname(name)}[k & 1][ty][tx] = {tgt};")
+                out.append(f"lds_{cname(name)}[k & {self.pmask}][ty][tx] = {tgt};")
             if self._mem(name):
                 st = mem_store(name, "k", tgt)
                 if name in self.api and self.tile:

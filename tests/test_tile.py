@@ -34,9 +34,11 @@ from stencil_cases import (  # noqa: E402  (the programs live with their referen
 )
 from stencil_cases import staged_forward_ij_temp as fwd_recurrence_ij_temp  # noqa: E402
 
-# (tile_by, tile_ti, tile_bx): block rows, tile width in I and block lanes in I (0: defaults,
-# the aligned tile width and 64 or 128 lanes by cell size)
-GEOMS = [(8, 0, 0), (4, 0, 0), (16, 0, 0), (8, 60, 64), (16, 13, 0), (4, 0, 128), (8, 100, 128)]
+# (tile_by, tile_ti, tile_bx[, tile_lblock]): block rows, tile width in I and block lanes in I (0:
+# defaults, the aligned tile width and 64 or 128 lanes by cell size), levels per LDS barrier
+# (default 2 when a loop can be blocked)
+GEOMS = [(8, 0, 0), (4, 0, 0), (16, 0, 0), (8, 60, 64), (16, 13, 0), (4, 0, 128), (8, 100, 128),
+         (8, 0, 0, 1), (4, 0, 0, 4), (16, 0, 0, 1), (8, 60, 64, 4)]
 
 # name: (definition, {field: (halo_i_lo, halo_i_hi, halo_j_lo, halo_j_hi)}, dtype)
 CASES = {name: (defn, halos, np.dtype(dt).type) for name, (defn, halos, dt) in TILE_PROGRAMS.items()}
@@ -140,8 +142,11 @@ GEOM_GOLDEN = [n for n in TILE_GOLDEN if n.endswith("_d131")] + FUZZ_GOLDEN[:4]
 
 
 def geom_opts(geom):
-    tile_by, tile_ti, tile_bx = geom
-    return {"tile_by": tile_by, "tile_ti": tile_ti, "tile_bx": tile_bx}
+    tile_by, tile_ti, tile_bx = geom[:3]
+    opts = {"tile_by": tile_by, "tile_ti": tile_ti, "tile_bx": tile_bx}
+    if len(geom) > 3:
+        opts["tile_lblock"] = geom[3]
+    return opts
 
 
 @pytest.mark.gpu
@@ -178,8 +183,7 @@ def test_tile_vs_numpy_backend(name, geom):
     arrays, origins = _inputs(name, domain, seed=sum(domain))
     ref = {k: v.copy() for k, v in arrays.items()}
     _stencil(name, "numpy")(**ref, origin=origins, domain=domain)
-    tile_by, tile_ti, tile_bx = geom
-    st = _stencil(name, "gt:mi355x", tile_by=tile_by, tile_ti=tile_ti, tile_bx=tile_bx)
+    st = _stencil(name, "gt:mi355x", **geom_opts(geom))
     dev = {k: storage.from_array(v, v.dtype, backend="gt:mi355x", aligned_index=origins[k]) for k, v in arrays.items()}
     st(**dev, origin=origins, domain=domain)
     got = storage.to_numpy(dev["out"])
