@@ -118,7 +118,6 @@ class Mi355xBackend(BaseBackend):
         "kreg": {"versioning": True, "type": int, "description": "column kernels: levels of the sweep-to-sweep tail cache held in registers (register band next to the LDS band)"},
         "kreg_pf": {"versioning": True, "type": int, "description": "column kernels: register-band levels whose memory fronts are loaded ahead (default: the load ring depth + 2; 0 = at their level)"},
         "ktail_head": {"versioning": True, "type": int, "description": "column kernels: keep the FIRST levels of the writer's sweep on chip (1), the last (0), or auto (-1: first for cached API outputs, last for write-free scratch)"},
-        "probe_nobar": {"versioning": True, "type": int, "description": "PROBE"},
         "col_bx": {"versioning": True, "type": int, "description": "column kernels: threads per block along I (64/128/256)"},
         "col_order": {"versioning": True, "type": int, "description": "column kernels: block order (0 natural, 1 xcd-aware, default)"},
         "jmirror": {"versioning": True, "type": int, "description": "plane kernels: odd J chunks stream top-down"},

@@ -849,7 +849,7 @@ class ColumnGen:
                                  if not w and isinstance(a, ir.FieldAccess) and a.name in self.lds
                                  and (a.offset[0] or a.offset[1])}
                         if reads & pending:
-                            body.append("gtmi::lds_barrier();  // the level's planes are complete" if not self.opts.get("probe_nobar") else "// probe: no barrier")
+                            body.append("gtmi::lds_barrier();  // the level's planes are complete")
                             pending.clear()
                     code = self._stmt(s, rend, wvar, mem_store)
                     g = self._guard(li, si, ti)
@@ -864,7 +864,7 @@ class ColumnGen:
                 if pending:
                     # planes written but not read across columns at this level: the next write of
                     # the same buffer (two levels on) must not overtake a slow reader
-                    body.append("gtmi::lds_barrier();" if not self.opts.get("probe_nobar") else "// probe: no barrier")
+                    body.append("gtmi::lds_barrier();")
                 if tail_write and band_now[0] == "reg":
                     body.append("// register band: this level's final values")
                     body += [f"rb_{cname(n)}_{reg_now[0]} = {wvar(n, 0, 0, 0)};" for n in tail_write]
