@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5: GPU suite + smoke on prebuilt libraries (tile level blocking in), PMC record of the new
+# staged library, then the default bench line.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r05m}
+mkdir -p $O
+GTMI_NO_COMPILE=1 GTMI_CACHE_LOG=$PWD/$O/build_keys.log bash scripts/gpu_tests.sh || exit $?
+cp gpurun_out/pytest_gpu.log gpurun_out/smoke.log $O/
+GTMI_NO_COMPILE=1 CONFIGS="staged" TAG=${TAG:-r05m} timeout -k 10 600 bash scripts/profile.sh > $O/profile.log 2>&1 || { tail -30 $O/profile.log; exit 1; }
+GTMI_NO_COMPILE=1 GTMI_CACHE_LOG=$PWD/$O/build_keys.log timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+cut -c1-300 $O/bench.json
