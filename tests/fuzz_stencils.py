@@ -55,9 +55,60 @@ class _Gen:
         return f"abs({x})"
 
 
+def _generate_v3(seed):
+    """Seeds >= 7000: the column-kernel schedules of round 5. A FORWARD sweep followed by a
+    BACKWARD sweep that reads the first one's products at (0, 0) -- a write-free scratch
+    temporary and/or an API output (sweep-to-sweep cache: tail placement for scratch, head
+    placement for API outputs, register band when nk is large) -- or a FORWARD recurrence whose
+    product a second FORWARD computation reads across columns (tile kernel, two levels per
+    barrier)."""
+    g = _Gen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    L = [f"def {name}(a: Field[np.float64], b: Field[np.float64], c: Field[np.float64], "
+         f"out1: Field[np.float64], out2: Field[np.float64], *, s: float):"]
+    if r.random() < 0.6:
+        temp, api = r.random() < 0.7, r.random() < 0.6
+        if not (temp or api):
+            temp = True
+        L.append("    with computation(FORWARD):")
+        L.append("        with interval(0, 1):")
+        if temp:
+            L.append(f"            cc = {g.expr(2, False, 'seq')}")
+        if api:
+            L.append(f"            out1 = {g.expr(2, False, 'seq')}")
+        L.append("        with interval(1, None):")
+        if temp:
+            L.append(f"            cc = cc[0, 0, -1] * 0.5 + {g.expr(2, False, 'seq')}")
+        if api:
+            L.append(f"            out1 = {g.expr(1, False, 'seq')} - out1[0, 0, -1] * 0.25")
+        rd = " + ".join((["cc"] if temp else []) + (["out1"] if api else []))
+        L.append("    with computation(BACKWARD):")
+        L.append("        with interval(-1, None):")
+        L.append(f"            out2 = {rd} * s")
+        L.append("        with interval(0, -1):")
+        L.append(f"            out2 = ({rd}) * 0.5 - out2[0, 0, 1] * 0.25 + {g.expr(1, False, 'seq')}")
+    else:
+        L.append("    with computation(FORWARD):")
+        L.append("        with interval(0, 1):")
+        L.append(f"            ss = {g.expr(2, False, 'seq')}")
+        L.append("        with interval(1, None):")
+        L.append(f"            ss = ss[0, 0, -1] * 0.5 + {g.expr(2, False, 'seq')}")
+        L.append("    with computation(FORWARD), interval(...):")
+        L.append(f"        tt = ss * {round(r.uniform(0.5, 2), 3)} + {g.expr(1, False, 'seq')}")
+        offs = [(1, 0), (-1, 0), (0, 1), (0, -1), (1, 1), (-1, -1)]
+        picks = r.sample(offs, r.randint(2, 4))
+        terms = " + ".join(f"tt[{di}, {dj}, 0]" for di, dj in picks)
+        L.append(f"        out1 = {terms} - ss * {g.expr(1, False, 'seq')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
-    cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering."""
+    cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
+    seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``."""
+    if seed >= 7000:
+        return _generate_v3(seed)
     v2 = seed >= 1000
     g = _Gen(seed)
     r = g.r

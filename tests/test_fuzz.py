@@ -16,13 +16,19 @@ from gt4py_amd.gtscript import BACKWARD, FORWARD, PARALLEL, Field, I, J, computa
 
 """
 SEEDS = list(range(60)) + list(range(1000, 1060))
-# stress runs: GTMI_FUZZ_EXTRA=N adds N more programs (seeds 5000...)
+# stress runs: GTMI_FUZZ_EXTRA=N adds N more programs (seeds 5000...), GTMI_FUZZ_V3=N adds N of
+# the sweep-pair / tile templates (seeds 7000...)
 SEEDS += list(range(5000, 5000 + int(os.environ.get("GTMI_FUZZ_EXTRA", "0"))))
+SEEDS += list(range(7000, 7000 + int(os.environ.get("GTMI_FUZZ_V3", "24"))))
 
 
 def _shape(seed):
-    # odd seeds: several 128-wide plane strips, several J chunks, a partial last chunk
-    return (13, 11, 8) if seed % 2 == 0 else (300, 45, 6)
+    # odd seeds: several 128-wide plane strips, several J chunks, a partial last chunk;
+    # GTMI_FUZZ_NK (stress runs) overrides the level count, e.g. 120 so that register bands,
+    # head/tail sweep caches and blocked tile levels are reached
+    nk = int(os.environ.get("GTMI_FUZZ_NK", "0"))
+    ni, nj, nk0 = (13, 11, 8) if seed % 2 == 0 else (300, 45, 6)
+    return ni, nj, nk or nk0
 
 
 def _opts(seed):
