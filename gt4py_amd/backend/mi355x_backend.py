@@ -124,7 +124,7 @@ class Mi355xBackend(BaseBackend):
         "row_unroll": {"versioning": True, "type": int, "description": "plane kernels: row steps per loop trip (ring rotations become renames; 0 = off, -1 = auto: 4 for small register state, default)"},
         "bufld": {"versioning": True, "type": int, "description": "plane kernels: interior strips load rows through buffer descriptors, branch-free, so prefetched rows stay in flight (1 on, 0 off, -1 auto: on for 4-cell lanes, default)"},
         "tile": {"versioning": True, "type": int, "description": "sequential sweeps that read their own products across columns: tile kernels with LDS planes (1, default) instead of the staged lowering (0)"},
-        "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per block (4, 8, 16)"},
+        "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per block (4, 8, 16; -1 auto, default: 16 for a one-row J halo on 8-byte cells, else 8)"},
         "tile_lblock": {"versioning": True, "type": int, "description": "tile kernels: levels per LDS barrier in the steady-state loop (1, 2, 4)"},
         "tile_bx": {"versioning": True, "type": int, "description": "tile kernels: I lanes per block (64 or 128)"},
         "tile_ti": {"versioning": True, "type": int, "description": "tile kernels: output columns per tile in I (default: 64 minus the sweep's I extent)"},

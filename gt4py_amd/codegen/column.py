@@ -50,7 +50,13 @@ AUTO_KREG_API_PF = 6
 # I-neighbour lane shifts (nbr_shfl) and split cached/uncached writer segments (seg_tail).
 BAND_PF_OVER_RING = 2
 DEFAULT_TAIL_HEAD = -1  # auto: see ColumnGen._plan_tail
-TILE_BY = 8  # tile mode: J rows of threads per block (64 or 128 lanes x 8, halo included)
+# tile mode: J rows of threads per block, halo included (option ``tile_by``; -1 = auto: 16 rows as
+# one 1024-thread block when the tile's J halo is a single row and its cells are 8 bytes, else 8).
+# A one-row halo costs a tile 1/8 of its rows at 8 and 1/16 at 16; with halo rows on both sides the
+# 1024-thread block's 128-VGPR cap costs more than the halved re-read saves (profiles/r05/
+# r05e_tile_probe.log, r05l_*: fwd_recurrence -4 %, staged -2.8 %; two_phase_chain, bwd_recurrence
+# and tile_f32 +1.5-4 % at 16)
+TILE_BY = -1
 # tile mode: levels per LDS barrier in the steady-state loop (a level's statements after the barrier
 # wait for the next level's before it; planes rotate over 2 x TILE_LBLOCK buffers). Every tile
 # program at 1024^2x80 (profiles/r05/r05l_tile_probe.log): tile_f32 -6 %, bwd_recurrence -1.8 %,
@@ -142,6 +148,8 @@ class ColumnGen:
         128 x 8 for narrower ones)."""
         if getattr(self.kernel, "tile", False):
             by = int(self.opts.get("tile_by", TILE_BY))
+            if by == -1:
+                by = 16 if self.ext[2] + self.ext[3] <= 1 and self._tile_item() >= 8 else 8
             # two waves per row for cells of 4 bytes or less (a row of 448 B of outputs, r03l sweep)
             bx = int(self.opts.get("tile_bx", 0)) or (128 if self._tile_item() <= 4 and by <= 8 else 64)
             if by not in (4, 8, 16) or bx not in (64, 128) or bx * by > 1024:

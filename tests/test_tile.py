@@ -77,6 +77,16 @@ def test_scratch_stores_of_tile_kernels_are_tile_local():
     assert store, "no tile-local guard in the tile kernel"
 
 
+@pytest.mark.parametrize("name,block", [("fwd_recurrence_ij_temp", "dim3(64, 16)"), ("tile_with_k_window", "dim3(64, 16)"),
+                                        ("two_phase_chain", "dim3(64, 8)"), ("bwd_recurrence_ij_temp", "dim3(64, 8)"),
+                                        ("tile_f32", "dim3(128, 8)")])
+def test_tile_rows_auto_rule(name, block):
+    """tile_by auto: 16 rows for a one-row J halo on 8-byte cells, else 8 (column.py TILE_BY)."""
+    src = _stencil(name, "gt:mi355x")._gt_run_impl_.compiled.source
+    assert block in src
+    assert _stencil(name, "gt:mi355x", tile_by=8)._gt_run_impl_.compiled.source.count("dim3(64, 16)") == 0
+
+
 def test_tile_off_uses_staged_lowering():
     st = _stencil("fwd_recurrence_ij_temp", "gt:mi355x", tile=0)
     plan = st._gt_run_impl_.compiled.plan
