@@ -19,7 +19,7 @@ import sys
 
 def counters(out, cfg):
     vals = {}
-    for p in ("A", "B", "C", "D"):
+    for p in ("A", "B", "C", "D", "E", "F"):
         for f in glob.glob(f"{out}/{cfg}_{p}/**/*counter_collection.csv", recursive=True):
             per = {}
             for r in csv.DictReader(open(f)):
@@ -55,6 +55,11 @@ def main():
         for f in ("SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL", "SQ_VMEM_WR_TA_DATA_FIFO_FULL"):
             if f in v and wc:
                 row[f.lower() + "_per_wave_cycle"] = round(v[f] / wc, 5)
+        ih, im = v.get("SQC_ICACHE_HITS"), v.get("SQC_ICACHE_MISSES")
+        if ih is not None and im is not None and ih + im:
+            row["icache_miss_rate"] = round(im / (ih + im), 4)
+        if v.get("SQ_IFETCH") and v.get("SQ_IFETCH_LEVEL") is not None:
+            row["ifetch_latency_quad_cycles"] = round(v["SQ_IFETCH_LEVEL"] / v["SQ_IFETCH"], 1)
         h, m = v.get("TCC_HIT_sum"), v.get("TCC_MISS_sum")
         if h is not None and m is not None and h + m:
             row["L2_hit"] = round(h / (h + m), 4)
