@@ -23,6 +23,13 @@ def main():
     ap.add_argument("--config", default="hdiff")
     ap.add_argument("--pre-gb", type=float, default=0.0, help="device memory held before the fields")
     ap.add_argument("--post-free", action="store_true", help="free the pre-allocation before timing")
+    ap.add_argument("--carve", action="store_true",
+                    help="free the pre-allocation BEFORE the fields: torch's caching allocator then carves "
+                         "the fields out of that one cached segment")
+    ap.add_argument("--warm-s", type=float, default=0.0,
+                    help="keep the GPU busy this long before the fields are allocated")
+    ap.add_argument("--warm-with", default="copy", help="'copy' (a torch device copy loop) or a bench config")
+    ap.add_argument("--empty-cache", action="store_true", help="release torch's cached blocks after the warm-up")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
 
@@ -30,9 +37,37 @@ def main():
 
     import bench
 
+    if args.warm_s > 0:
+        import time
+
+        if args.warm_with == "copy":
+            a = torch.empty(1 << 30, dtype=torch.float32, device="cuda")
+            b = torch.empty_like(a)
+            step = lambda: b.copy_(a)  # noqa: E731
+        else:
+            ns0 = types.SimpleNamespace(decomp="jstrips", jchunk=None, opt=None, fill="bulk", no_overlap=False,
+                                        halo_selfcomm=False)
+            wl0 = bench.Workload(args.warm_with, ns0, 0, 1, torch.device("cuda", 0), "gt:mi355x")
+            step = wl0.plain_step
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.warm_s:
+            for _ in range(20):
+                step()
+            torch.cuda.synchronize()
+        del step
+        if args.warm_with == "copy":
+            del a, b
+        else:
+            del wl0
+        if args.empty_cache:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
     pre = None
     if args.pre_gb > 0:
         pre = torch.empty(int(args.pre_gb * (1 << 30)), dtype=torch.uint8, device="cuda")
+        if args.carve:
+            del pre
+            pre = None
     ns = types.SimpleNamespace(decomp="jstrips", jchunk=None, opt=None, fill="bulk", no_overlap=False,
                                halo_selfcomm=False)
     wl = bench.Workload(args.config, ns, 0, 1, torch.device("cuda", 0), "gt:mi355x")
@@ -49,8 +84,8 @@ def main():
         b.record()
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in evs)
-    rec = {"tag": args.tag, "pre_gb": args.pre_gb, "kernel_ms": round(ms[len(ms) // 2], 4),
-           "ptrs": {k: hex(t.data_ptr()) for k, t in (wl.named or {}).items()}}
+    rec = {"tag": args.tag, "config": args.config, "pre_gb": args.pre_gb, "carve": args.carve, "warm_s": args.warm_s, "warm_with": args.warm_with, "empty_cache": args.empty_cache, "kernel_ms": round(ms[len(ms) // 2], 4),
+           "ptrs": [hex(t.data_ptr()) for t in wl.args if hasattr(t, "data_ptr")]}
     rec["placement_probe"] = (wl.placement or {}).get("candidates_ms")
     print(json.dumps(rec), flush=True)
 
