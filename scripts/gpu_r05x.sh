@@ -14,7 +14,10 @@ P1="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUE
 P2="TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum"
 P3="FETCH_SIZE"
 P4="SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"
-for p in 1 2 3 4; do
+P5="GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"
+P6="TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_PENDING_STALL_CYCLES_sum"
+P7="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_LEVEL_sum"
+for p in ${PASSES:-1 2 3 4}; do
   eval "ctrs=\$P$p"
   timeout -s KILL 180 rocprofv3 --pmc $ctrs --output-format csv -d $O/p$p -o pmc -- \
     python3 scripts/column_placement_probe.py --config $C --sets $S --reps $R > $O/p$p.json 2> $O/p$p.err || { tail -20 $O/p$p.err; exit 1; }
