@@ -43,15 +43,66 @@ def summarize(dirs, sets, reps):
     print(json.dumps({"per_dispatch_by_set": out}, indent=1))
 
 
+def _time(call, reps):
+    import torch
+
+    call()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record()
+        call()
+        b.record()
+    torch.cuda.synchronize()
+    t = sorted(a.elapsed_time(b) for a, b in evs)
+    return round(t[len(t) // 2], 4)
+
+
+def build_variants(args):
+    import bench
+    from gt4py_amd import gtscript
+
+    variants = []
+    for part in filter(None, (p.strip() for p in args.variants.split(";"))):
+        variants.append({k.strip(): int(v) for k, v in (kv.split("=") for kv in part.split(","))} if "=" in part else {})
+    sname, dtype = bench.CONFIGS[args.config][:2]
+    sts = [gtscript.stencil(backend="gt:mi355x", definition=bench.stencil_defs()[(sname, dtype)],
+                            name=f"cpp.{args.config}.{i}", device_sync=False,
+                            externals=bench.EXTERNALS.get(sname, {}), **v) for i, v in enumerate(variants)]
+    return variants, sts
+
+
+def variant_matrix(args, wl, sets):
+    variants, sts = build_variants(args)
+    rows = []
+    for si, s in enumerate(sets):
+        for st in sts:  # first call: validation on this set
+            st(*s, **wl.params, origin=wl.origin, domain=wl.domain)
+        ms = [[] for _ in sts]
+        for _ in range(args.rounds):
+            for i, st in enumerate(sts):
+                ms[i].append(_time(lambda st=st, s=s: st(*s, **wl.params, origin=wl.origin, domain=wl.domain,
+                                                           validate_args=False), args.reps))
+        rows.append({"set": si, "ms": [sorted(m)[len(m) // 2] for m in ms]})
+        print(json.dumps(rows[-1]), flush=True)
+    print(json.dumps({"config": args.config, "variants": variants, "matrix": [r["ms"] for r in rows]}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="tridiag")
     ap.add_argument("--sets", type=int, default=6)
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--summarize", nargs="*", default=None)
+    ap.add_argument("--variants", default="",
+                    help="codegen option sets 'k=v,k=v;k=v' timed on every placement set, interleaved "
+                         "(a variant matrix: which schedule wins in which placement mode)")
+    ap.add_argument("--build-only", action="store_true", help="compile the --variants libraries (no GPU)")
     args = ap.parse_args()
     if args.summarize is not None:
         return summarize(args.summarize, args.sets, args.reps)
+    if args.build_only:
+        return print(f"built {len(build_variants(args)[1])} variants")
     import torch
 
     import bench
@@ -73,6 +124,8 @@ def main():
                 s.append(a)
         sets.append(s)
     torch.cuda.synchronize()
+    if args.variants:
+        return variant_matrix(args, wl, sets)
     res = []
     for s in sets:
         call = lambda s=s: wl.stencil(*s, **wl.params, origin=wl.origin, domain=wl.domain,  # noqa: E731
