@@ -736,7 +736,7 @@ def sharded_leg(cfg, args, rank, world, dev, backend, dist) -> dict:
     rec = {
         "workload": f"{w.sname} {ni}x{nj}x{nk} {np.dtype(w.dtype).name} per GPU, "
                     f"{'J-strips' if w.dec2d is None else f'{w.dec2d.pi}x{w.dec2d.pj} tiles'} of a "
-                    f"{gi}x{gj}x{nk} global domain, RCCL halo {w.h}",
+                    f"{gi}x{gj}x{nk} global domain, {halo_transport(dist)} halo {w.h}",
         "n_gpus": world,
         "global_domain": [gi, gj, nk],
         "steps": steps,
@@ -791,6 +791,12 @@ class RankPhase:
                              f"{self.limit:.0f} s (phases so far: {self.history}); exiting with status 3\n")
             sys.stderr.flush()
             os._exit(3)
+
+
+def halo_transport(dist) -> str:
+    """What moves the halos: RCCL (backend "nccl") or gloo through host memory (CPU rehearsals,
+    ranks sharing one GPU)."""
+    return "RCCL" if str(dist.get_backend()).lower() == "nccl" else "gloo (host-staged)"
 
 
 def probe_peers(rank, world, dec2d, selfcomm=False):
@@ -1071,7 +1077,7 @@ def main():
             "workload": f"{wl.sname} {ni}x{nj}x{nk} {np.dtype(wl.dtype).name} per GPU"
             + (
                 f", {'J-strips' if dec2d is None else f'{dec2d.pi}x{dec2d.pj} tiles'} of a "
-                f"{wl.global_ij[0]}x{wl.global_ij[1]}x{nk} global domain, RCCL halo {wl.h}"
+                f"{wl.global_ij[0]}x{wl.global_ij[1]}x{nk} global domain, {halo_transport(dist)} halo {wl.h}"
                 if world > 1
                 else ""
             ),

@@ -41,6 +41,8 @@ def test_bench_launcher_dry_run(gpus, decomp):
     assert rec["hbm_estimate"]["peak_gb"] >= rec["hbm_estimate"]["fields_gb"] > 0
     if gpus > 1:
         assert rec["config"]["parallelism"].startswith("ij-")
+        # the line names what moved the halos (the dry run's gloo, RCCL on the GPU nodes)
+        assert rec["config"]["workload"].endswith("gloo (host-staged) halo 2"), rec["config"]["workload"]
         if decomp == "2d":  # a balanced process grid: 2x2 at 4 ranks, 2x4 at 8
             want = {2: "1x2", 4: "2x2", 8: "2x4"}.get(gpus)
             if want is not None:
