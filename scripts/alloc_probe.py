@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--warm-s", type=float, default=0.0,
                     help="keep the GPU busy this long before the fields are allocated")
     ap.add_argument("--warm-with", default="copy", help="'copy' (a torch device copy loop) or a bench config")
+    ap.add_argument("--pre-chunks", type=int, default=0, help="hold this many --pre-chunk-gb blocks before the fields")
+    ap.add_argument("--pre-chunk-gb", type=float, default=1.5)
     ap.add_argument("--empty-cache", action="store_true", help="release torch's cached blocks after the warm-up")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
@@ -62,6 +64,8 @@ def main():
         if args.empty_cache:
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+    held = [torch.empty(int(args.pre_chunk_gb * (1 << 30)), dtype=torch.uint8, device="cuda")
+            for _ in range(args.pre_chunks)]
     pre = None
     if args.pre_gb > 0:
         pre = torch.empty(int(args.pre_gb * (1 << 30)), dtype=torch.uint8, device="cuda")
@@ -84,7 +88,8 @@ def main():
         b.record()
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in evs)
-    rec = {"tag": args.tag, "config": args.config, "pre_gb": args.pre_gb, "carve": args.carve, "warm_s": args.warm_s, "warm_with": args.warm_with, "empty_cache": args.empty_cache, "kernel_ms": round(ms[len(ms) // 2], 4),
+    rec = {"tag": args.tag, "config": args.config, "pre_gb": args.pre_gb, "carve": args.carve, "warm_s": args.warm_s, "warm_with": args.warm_with, "empty_cache": args.empty_cache, "pre_chunks": args.pre_chunks,
+           "pre_chunk_gb": args.pre_chunk_gb, "held": len(held), "kernel_ms": round(ms[len(ms) // 2], 4),
            "ptrs": [hex(t.data_ptr()) for t in wl.args if hasattr(t, "data_ptr")]}
     rec["placement_probe"] = (wl.placement or {}).get("candidates_ms")
     print(json.dumps(rec), flush=True)
