@@ -469,12 +469,23 @@ def box_identity(dev_index: int = 0):
 # ------------------------------------------------------------------------------------------
 
 
-def hbm_estimate(stencil, args, candidates) -> dict:
+# placement tuning scope per config (--placement-scope auto): the column kernels (one wave per SIMD,
+# latency-bound on every stream they read) re-home all their fields, the plane and tile kernels
+# the written ones (DESIGN.md §5 "the column kernels have placement modes too")
+PLACEMENT_SCOPE = {"tridiag": "all", "vadv": "all"}
+
+
+def placement_scope(cfg, args) -> str:
+    scope = getattr(args, "placement_scope", "auto")
+    return PLACEMENT_SCOPE.get(cfg, "written") if scope == "auto" else scope
+
+
+def hbm_estimate(stencil, args, candidates, scope="written") -> dict:
     """Peak device memory of one rank for this config (bytes, from the allocated fields): the
     fields themselves, and the placement tuner's transient copies of the fields the stencil writes
     (a backup plus ``candidates`` buffer sets, each padded by 2 MiB; the tuner itself caps the sets
     at 80 % of free memory); the halo path's pack buffers are faces, negligible. DESIGN.md §6."""
-    from gt4py_amd.storage.placement import written_fields
+    from gt4py_amd.storage.placement import scope_fields
 
     def nbytes(t):
         try:
@@ -484,8 +495,8 @@ def hbm_estimate(stencil, args, candidates) -> dict:
 
     names = list(stencil.field_info)
     fields = sum(nbytes(t) for t in args)
-    written = set(written_fields(stencil))
-    per_set = sum(nbytes(t) + (2 << 20) for n, t in zip(names, args) if n in written)
+    tuned = set(scope_fields(stencil, scope))
+    per_set = sum(nbytes(t) + (2 << 20) for n, t in zip(names, args) if n in tuned)
     tuner = (1 + candidates) * per_set if candidates > 0 else 0
     return {"fields_gb": round(fields / 1e9, 6), "tuner_transient_gb": round(tuner / 1e9, 6),
             "peak_gb": round((fields + tuner) / 1e9, 6)}
@@ -601,7 +612,8 @@ class Workload:
         self.stencil(*self.args, **self.params, origin=self.origin, domain=self.domain)
         self.placement = None
         self.untuned = None
-        self.hbm_estimate = hbm_estimate(self.stencil, self.args, getattr(args, "placement_candidates", 0))
+        self.hbm_estimate = hbm_estimate(self.stencil, self.args, getattr(args, "placement_candidates", 0),
+                                         placement_scope(cfg, args))
         ncand = getattr(args, "placement_candidates", 0)
         if not dry_run and ncand > 0:
             self.tune_placement(ncand, args)
@@ -618,6 +630,7 @@ class Workload:
         self.untuned = {"ms_per_step": el / steps * 1e3, "kernel_ms": km}
         try:
             self.placement = self.stencil.tune_placement(*self.args, **self.params, origin=self.origin,
+                                                         scope=placement_scope(self.cfg, args),
                                                          domain=self.domain, candidates=candidates)
         except (ValueError, RuntimeError, TypeError) as e:
             # a refusal (e.g. a viewed or weakly referenced written field) leaves the first
@@ -906,6 +919,9 @@ def main():
                     help="before timing, place the fields the stencil writes in the fastest of this many other "
                          "buffer sets besides the first allocation (gt4py_amd.storage.placement; 0 = off, the "
                          "first allocation is timed)")
+    ap.add_argument("--placement-scope", default="auto", choices=["auto", "written", "all"],
+                    help="fields the placement tuner re-homes: auto (all fields for the column-kernel configs "
+                         "tridiag and vadv, the written ones otherwise), written, or all")
     ap.add_argument("--opt", action="append", default=None, metavar="KEY=VALUE",
                     help="gt:mi355x codegen option for the headline config (repeatable)")
     ap.add_argument("--fill", default="bulk", choices=["slab", "bulk"],
@@ -1113,7 +1129,7 @@ def main():
                                   frac_untuned=round(u_gbs / HBM_PEAK_GBS, 4),
                                   untuned_ms_per_step=round(wl.untuned["ms_per_step"], 4),
                                   Mcells_s_untuned=round(cells_per_step / (wl.untuned["ms_per_step"] * 1e-3) / 1e6, 2),
-                                  tuned_note="kernel_ms/frac: written fields re-homed in place by the opt-in "
+                                  tuned_note="kernel_ms/frac: fields re-homed in place by the opt-in "
                                              "StencilObject.tune_placement (DESIGN.md §5); *_untuned: the first "
                                              "allocation, same K-step measurement")
     result["hbm_estimate"] = dict(wl.hbm_estimate, per_rank=True)
@@ -1151,8 +1167,9 @@ def main():
     if wl.placement is not None:
         # the written fields were placed by measurement before the timed steps: every buffer set's
         # kernel time (set 0 = the first allocation, i.e. the untuned time) and the one chosen
-        result["placement"] = dict(wl.placement, note="written fields in the fastest of the measured buffer sets "
-                                   "(gt4py_amd.storage.placement, DESIGN.md §5); set 0 is the first allocation")
+        result["placement"] = dict(wl.placement, note="the fields of `scope` (written ones, or all) in the fastest "
+                                   "of the measured buffer sets (gt4py_amd.storage.placement, DESIGN.md §5); "
+                                   "set 0 is the first allocation")
     if box is not None:
         box["after"] = card_snapshot(find_card(box["identity"]["pci"]))
         # the fields' virtual addresses modulo 2 MiB and 1 GiB (physical addresses are not visible
@@ -1194,8 +1211,8 @@ def main():
                     "library": w.library_key(),
                 }
                 if w.placement is not None:
-                    extra[cfg]["placement"] = {k: w.placement.get(k) for k in ("candidates_ms", "chosen", "untuned_ms",
-                                                                               "error") if k in w.placement}
+                    extra[cfg]["placement"] = {k: w.placement.get(k) for k in ("scope", "candidates_ms", "chosen",
+                                                                               "untuned_ms", "error") if k in w.placement}
                 if w.untuned is not None and w.untuned["kernel_ms"]:
                     u_gbs = n_i * n_j * n_k * w.bpc / (w.untuned["kernel_ms"] * 1e-3) / 1e9
                     extra[cfg]["kernel_ms_untuned"] = round(w.untuned["kernel_ms"], 4)

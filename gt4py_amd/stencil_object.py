@@ -203,18 +203,20 @@ class FrozenStencil:
         object.__setattr__(self, "_fast", ns["_fast"])
         _frozen_set()[id(self)] = self
 
-    def tune_placement(self, *, candidates: int = 3, reps: int = 10, **kwargs) -> Dict[str, Any]:
-        """Re-home the fields this stencil writes, in place, to the fastest of ``candidates + 1``
-        HBM buffer sets for this frozen domain/origin (``storage.placement.tune_in_place``):
-        takes the keyword arguments of a call; the tensors stay the same objects. Returns the
-        report (every set's kernel time, set 0 = the current allocation)."""
+    def tune_placement(self, *, candidates: int = 3, reps: int = 10, scope: str = "written",
+                       **kwargs) -> Dict[str, Any]:
+        """Re-home the fields this stencil writes (``scope="all"``: all its fields), in place, to
+        the fastest of ``candidates + 1`` HBM buffer sets for this frozen domain/origin
+        (``storage.placement.tune_in_place``): takes the keyword arguments of a call; the tensors
+        stay the same objects. Returns the report (every set's kernel time, set 0 = the current
+        allocation)."""
         from gt4py_amd.storage.placement import tune_in_place
 
         so = self.stencil_object
         fields = {n: kwargs[n] for n in so.field_info}
         params = {n: kwargs[n] for n in so.parameter_info if n in kwargs}
         return tune_in_place(so, fields, origin=self.origin, domain=self.domain, params=params,
-                             candidates=candidates, reps=reps)
+                             candidates=candidates, reps=reps, scope=scope)
 
     def __call__(self, **kwargs) -> None:
         if self._fast(kwargs):  # exactly the field and parameter arguments, a prepared launch
@@ -633,10 +635,11 @@ class StencilObject(abc.ABC):
         return cls(self, origin, domain)
 
     def tune_placement(self, *args, candidates: int = 3, reps: int = 10, origin=None, domain=None,
-                       **kwargs) -> Dict[str, Any]:
+                       scope: str = "written", **kwargs) -> Dict[str, Any]:
         """Opt-in HBM placement for the drop-in path (DESIGN.md §5 "HBM placement"): called with
-        the arguments of an ordinary call, it re-homes the fields the stencil writes IN PLACE to
-        the fastest of ``candidates + 1`` buffer sets (``storage.placement.tune_in_place``) --
+        the arguments of an ordinary call, it re-homes the fields the stencil writes (``scope=
+        "all"``: every field it accesses, for column stencils whose read streams decide too) IN
+        PLACE to the fastest of ``candidates + 1`` buffer sets (``storage.placement.tune_in_place``) --
         the caller's tensors stay the same objects with the same contents, on other pages. Once,
         after allocating the fields; returns the report (every set's kernel time in ms, set 0 =
         the current allocation)."""
@@ -649,7 +652,7 @@ class StencilObject(abc.ABC):
         fields = {n: v for n, v in bound.arguments.items() if n in self.field_info}
         params = {n: v for n, v in bound.arguments.items() if n in self.parameter_info}
         return tune_in_place(self, fields, origin=origin, domain=domain, params=params, candidates=candidates,
-                             reps=reps)
+                             reps=reps, scope=scope)
 
     def clean_call_args_cache(self) -> None:
         type(self)._domain_origin_cache.clear()

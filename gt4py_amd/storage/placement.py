@@ -55,6 +55,19 @@ def written_fields(stencil) -> List[str]:
     return [n for n, fi in stencil.field_info.items() if fi is not None and fi.access & AccessKind.WRITE]
 
 
+def scope_fields(stencil, scope: str) -> List[str]:
+    """The fields a tuning run re-homes: ``"written"`` (the default; what decides a plane
+    kernel's placement mode) or ``"all"`` API fields the stencil accesses (a column kernel at one
+    wave per SIMD is latency-bound on every stream it reads: vadv, 1 written field of 5, stays
+    ~12 % slow on a fresh process's first allocation however its written field is placed;
+    DESIGN.md §5 "the column kernels have placement modes too")."""
+    if scope == "written":
+        return written_fields(stencil)
+    if scope == "all":
+        return [n for n, fi in stencil.field_info.items() if fi is not None]
+    raise ValueError(f"placement scope must be 'written' or 'all', got {scope!r}")
+
+
 def _time_call(call, reps: int) -> float:
     import torch
 
@@ -84,8 +97,8 @@ def tune_written_fields(
     in the fastest of ``candidates + 1`` buffer sets (set 0 = the given arrays).
 
     Returns ``(arrays, report)``: ``arrays`` maps every name to the field to use from now on (the
-    read-only ones unchanged), ``report`` = ``{"written", "candidates_ms", "chosen", "untuned_ms",
-    "tuned_ms"}``. Written fields keep their contents. Raises ``ValueError`` if a written field
+    read-only ones unchanged), ``report`` = ``{"written", "fields", "candidates_ms", "chosen",
+    "untuned_ms", "tuned_ms"}``. Written fields keep their contents. Raises ``ValueError`` if a written field
     shares memory with another argument (re-homing it would break the aliasing) and ``TypeError``
     for non-device arrays; fewer sets are tried when free device memory is short.
     """
@@ -121,8 +134,9 @@ def tune_fields(
         for m, u in arrays.items():
             if m != n and isinstance(u, torch.Tensor) and u.is_cuda and \
                     u.untyped_storage().data_ptr() == t.untyped_storage().data_ptr():
-                raise ValueError(f"tune_written_fields: written field '{n}' shares memory with '{m}'")
-    report: Dict[str, Any] = {"written": names, "candidates_ms": [], "chosen": 0}
+                raise ValueError(f"tune_written_fields: field '{n}' shares memory with '{m}'")
+    report: Dict[str, Any] = {"written": [n for n in written_fields(stencil) if n in names], "fields": names,
+                              "candidates_ms": [], "chosen": 0}
 
     def call_with(sub):
         a = dict(arrays)
@@ -209,9 +223,10 @@ def tune_in_place(
     candidates: int = 3,
     reps: int = 10,
     memory_fraction: float = 0.8,
+    scope: str = "written",
 ) -> Dict[str, Any]:
-    """:func:`tune_written_fields`, then move each written field the tuner re-homed into the
-    CALLER'S tensor object (``torch.utils.swap_tensors``): same object, same sizes, strides,
+    """:func:`tune_written_fields` (``scope="all"``: :func:`tune_fields` over every API field,
+    :func:`scope_fields`), then move each field the tuner re-homed into the CALLER'S tensor object (``torch.utils.swap_tensors``): same object, same sizes, strides,
     dtype and contents, new buffer; the old buffer is freed. Returns the report (with
     ``"in_place": True``).
 
@@ -222,13 +237,13 @@ def tune_in_place(
     """
     import torch
 
-    names = written_fields(stencil)
+    names = scope_fields(stencil, scope)
     for n in names:
         t = arrays.get(n)
         if not (type(t) is torch.Tensor and t.is_cuda):
             raise TypeError(f"tune_placement: '{n}' is not a plain device torch.Tensor")
         if not _exclusive(t):
-            raise ValueError(f"tune_placement: written field '{n}' shares its storage with other tensors "
+            raise ValueError(f"tune_placement: field '{n}' shares its storage with other tensors "
                              f"(views would keep the old buffer); use tune_written_fields and pass the returned arrays")
     # weak references held outside gt4py_amd: refused before anything is timed (our own prepared
     # launches and packed-argument caches are dropped first; they re-prepare on the next call)
@@ -241,8 +256,9 @@ def tune_in_place(
     if held:
         raise RuntimeError(f"tune_placement: field(s) {held} are weakly referenced elsewhere; cannot re-home "
                            "them in place (use tune_written_fields)")
-    out, report = tune_written_fields(stencil, arrays, origin=origin, domain=domain, params=params,
-                                      candidates=candidates, reps=reps, memory_fraction=memory_fraction)
+    out, report = tune_fields(stencil, arrays, names, origin=origin, domain=domain, params=params,
+                              candidates=candidates, reps=reps, memory_fraction=memory_fraction)
+    report["scope"] = scope
     moved = [n for n in names if out[n] is not arrays[n]]
     if moved:
         drop_prepared_launches()  # the tuner's own timing calls prepared launches again

@@ -20,6 +20,10 @@ def test_written_fields_from_field_info():
     td = gtscript.stencil(backend="numpy", definition=case.definition, externals=case.externals,
                           name="placement.tridiag")
     assert placement.written_fields(td) == ["sup", "rhs", "out"]
+    assert placement.scope_fields(td, "written") == ["sup", "rhs", "out"]
+    assert placement.scope_fields(td, "all") == list(td.field_info)
+    with pytest.raises(ValueError, match="scope"):
+        placement.scope_fields(td, "read")
 
 
 def test_like_keeps_layout_and_residue():
@@ -136,9 +140,10 @@ def _dev_case(name, st):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["hdiff_f64", "tridiag"])
-@pytest.mark.parametrize("frozen", [False, True])
-def test_tune_placement_in_place_drop_in(name, frozen):
+@pytest.mark.parametrize("name,frozen,scope", [("hdiff_f64", False, "written"), ("hdiff_f64", True, "written"),
+                                               ("tridiag", False, "written"), ("tridiag", True, "written"),
+                                               ("tridiag", False, "all"), ("vertical_advection_dycore", True, "all")])
+def test_tune_placement_in_place_drop_in(name, frozen, scope):
     """``StencilObject.tune_placement`` / ``FrozenStencil.tune_placement`` with the arguments of
     an ordinary call: the caller's tensors stay the same objects with the same contents, the
     written ones on the chosen buffers; a prepared launch made before tuning is dropped, and the
@@ -167,17 +172,18 @@ def test_tune_placement_in_place_drop_in(name, frozen):
         fz(**dev, **case.params)
         for k, v in host.items():
             dev[k].copy_(torch.from_numpy(np.ascontiguousarray(v)).to(dev[k].device))
-        rep = fz.tune_placement(**dev, **case.params, candidates=2, reps=2)
+        rep = fz.tune_placement(**dev, **case.params, candidates=2, reps=2, scope=scope)
     else:
-        rep = st.tune_placement(**dev, **case.params, **kw, candidates=2, reps=2)
+        rep = st.tune_placement(**dev, **case.params, **kw, candidates=2, reps=2, scope=scope)
     assert rep["in_place"] and len(rep["candidates_ms"]) == 3 and rep["written"] == placement.written_fields(st)
+    assert rep["scope"] == scope and rep["fields"] == placement.scope_fields(st, scope)
     for k, v in dev.items():
         assert id(v) == ids[k]
         gu.assert_match(storage.to_numpy(v), host[k], name=f"{name}:{k} contents kept")
-        if k not in rep["written"]:
+        if k not in rep["fields"]:
             assert v.data_ptr() == ptrs[k]
     if rep["chosen"] != 0:
-        assert any(dev[k].data_ptr() != ptrs[k] for k in rep["written"])
+        assert all(dev[k].data_ptr() != ptrs[k] for k in rep["fields"])
     if frozen:
         fz(**dev, **case.params)
     else:
@@ -213,10 +219,11 @@ def test_tune_placement_in_place_refusals():
     def no_timing(*a_, **k_):
         raise AssertionError("refused only after timing (ADVICE r04)")
 
-    saved, placement.tune_written_fields = placement.tune_written_fields, no_timing
+    saved = placement.tune_written_fields, placement.tune_fields
+    placement.tune_written_fields = placement.tune_fields = no_timing
     try:
         with pytest.raises(RuntimeError, match="weakly referenced"):  # before anything is timed
             st.tune_placement(**{names[0]: a, names[1]: b}, origin=(0, 0, 0), domain=(8, 8, 4), candidates=2, reps=1)
     finally:
-        placement.tune_written_fields = saved
+        placement.tune_written_fields, placement.tune_fields = saved
     assert ref() is b and b.data_ptr() == ptr
