@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 5: after pruning the in-tree cache to what build() prebuilds: GPU suite + smoke + the
+# default bench line, nothing compiled on the box.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r05zj}
+mkdir -p $O
+GTMI_NO_COMPILE=1 GTMI_CACHE_LOG=$PWD/$O/build_keys.log bash scripts/gpu_tests.sh || exit $?
+cp gpurun_out/pytest_gpu.log gpurun_out/smoke.log $O/
+GTMI_NO_COMPILE=1 GTMI_CACHE_LOG=$PWD/$O/build_keys.log timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+cut -c1-200 $O/bench.json
