@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5: more candidate sets for the all-field-tuned column configs (5 vs 9), default bench
 # lines alternating in separate processes on one box.
+# (--placement-candidates-all was a trial option of bench.py, removed again after this call)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
