@@ -19,7 +19,8 @@ same library (build key), else null. ``sustained`` (N=1): the same step repeated
 the timed K steps (steady-state ms/step; ``--sustain 0`` skips it). ``full_call`` (N=1): K calls
 the reference's way (validate_args=True, synchronize after each). ``extra_configs`` (N=1): the
 other BASELINE configs timed in the same process. ``cpu_baseline`` = the C restatement (cpu_ifirst-equivalent, OpenMP) on
-the full domain, median of 20 after 3 warm-ups, in a child process.
+the full domain, median of 40 after 3 warm-ups, in a child process; lap5 (C2) and tridiag (C4)
+carry their own ``extra_configs.<cfg>.cpu_baseline`` (median of 20) next to their GPU figures.
 """
 
 
@@ -254,11 +255,14 @@ def _demo_field(ni, nj, nk, dtype):
     return arr
 
 
-def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
-    """Body of the ``--cpu-child`` process: time the C oracle on the config's full domain."""
+def cpu_child(cfg_name: str, reps: int, warm: int, domain=None) -> dict:
+    """Body of the ``--cpu-child`` process: time the C oracle on the config's full domain
+    (``domain`` overrides it only for the CPU rehearsal of the dry run)."""
     from oracle import c_oracle
 
     sname, dtype, (ni, nj, nk), h, bpc = CONFIGS[cfg_name]
+    if domain is not None:
+        ni, nj, nk = domain
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     rng = np.random.default_rng(1337)
 
@@ -340,7 +344,9 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
         med2 = median_s(second[1])
         rec["second_input"] = {"inputs": second[0], "value": round(cells / med2 / 1e6, 2), "unit": "Mcells/s",
                                "ms_per_call": round(med2 * 1e3, 3)}
-    if sname == "horizontal_diffusion" and threads > 1:
+    if domain is not None:
+        rec["dry_run_domain"] = list(domain)
+    if sname == "horizontal_diffusion" and threads > 1 and domain is None:
         # thread scaling of the same code on a K-slab sample: the pool's rules
         # cap a one-GPU job at its CPU share, so the all-core figure is not run; the curve up to the
         # share says how the figure grows with cores
@@ -360,7 +366,7 @@ def cpu_child(cfg_name: str, reps: int, warm: int) -> dict:
     return rec
 
 
-def cpu_baseline(cfg_name: str, reps: int = 40, warm: int = 3, timeout_s: float = 240.0):
+def cpu_baseline(cfg_name: str, reps: int = 40, warm: int = 3, timeout_s: float = 240.0, domain=None):
     """Run ``cpu_child`` in a child process (fresh OpenMP runtime with the placement variables)."""
     import subprocess
 
@@ -386,6 +392,8 @@ def cpu_baseline(cfg_name: str, reps: int = 40, warm: int = 3, timeout_s: float 
     env["OMP_PLACES"] = "cores"
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", cfg_name, "--cpu-reps", str(reps),
            "--cpu-warm", str(warm)]
+    if domain is not None:
+        cmd += ["--cpu-domain", "x".join(str(int(n)) for n in domain)]
     try:
         res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
     except subprocess.TimeoutExpired:
@@ -718,6 +726,9 @@ def traffic_for(cfg, key):
     return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_{cfg}.json (library {key})"
 
 
+# N=1: configs that also get a cpu_ifirst-equivalent figure of their own in extra_configs
+CPU_EXTRA_CONFIGS = ("lap5", "tridiag")
+DRY_RUN_CPU_DOMAIN = (64, 32, 8)
 EXTRA_CONFIGS = ("lap5", "tridiag", "hdiff_f32", "copy", "vadv", "hdiff_blocks", "staged")
 C5_CONFIG = "hdiff_f32"  # BASELINE configs[4]: 8192x1024x160 f32 per GPU, J strips, RCCL halo
 
@@ -938,11 +949,13 @@ def main():
     ap.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-reps", type=int, default=40, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-warm", type=int, default=3, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-domain", default=None, help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 
     if args.cpu_child:
-        print(json.dumps(cpu_child(args.cpu_child, args.cpu_reps, args.cpu_warm)), flush=True)
+        dom = tuple(int(n) for n in args.cpu_domain.split("x")) if args.cpu_domain else None
+        print(json.dumps(cpu_child(args.cpu_child, args.cpu_reps, args.cpu_warm, dom)), flush=True)
         return 0
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -1227,6 +1240,22 @@ def main():
         cb = cpu_baseline(args.config)
         if cb:
             result["cpu_baseline"] = cb
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_extra and not args.halo_selfcomm:
+        # BASELINE configs[1] reads "1xMI355X vs gt:cpu_ifirst" (C2) and C4 is the hot path's
+        # K sweep: the same C restatement, thread policy and input distributions beside their GPU
+        # figures (the dry run rehearses the plumbing on a small domain)
+        extra = result.setdefault("extra_configs", {})
+        for cfg in CPU_EXTRA_CONFIGS:
+            if cfg == args.config:
+                continue
+            if args.dry_run:
+                cb = cpu_baseline(cfg, reps=3, warm=1, domain=DRY_RUN_CPU_DOMAIN)
+            else:
+                cb = cpu_baseline(cfg, reps=20)
+            entry = extra.setdefault(cfg, {})
+            entry["cpu_baseline"] = cb
+            if "kernel_ms" in entry and cb.get("ms_per_call"):
+                entry["gpu_vs_cpu"] = round(cb["ms_per_call"] / entry["kernel_ms"], 1)
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if dist is not None:

@@ -127,6 +127,7 @@ class Mi355xBackend(BaseBackend):
         "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per block (4, 8, 16; -1 auto, default: 16 for a one-row J halo on 8-byte cells, else 8)"},
         "tile_lblock": {"versioning": True, "type": int, "description": "tile kernels: levels per LDS barrier in the steady-state loop (1, 2, 4)"},
         "tile_bx": {"versioning": True, "type": int, "description": "tile kernels: I lanes per block (64 or 128)"},
+        "tile_order": {"versioning": True, "type": int, "description": "tile kernels: work order of the tiles within an XCD's range (0 I-fast, default; 1 J-fast; 2 pairs of J rows, I-fast)"},
         "tile_ti": {"versioning": True, "type": int, "description": "tile kernels: output columns per tile in I (default: 64 minus the sweep's I extent)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},

@@ -66,6 +66,7 @@ TILE_LBLOCK = 2
 _KVAR = re.compile(r"\bk\b")
 _WVAR = re.compile(r"\bw\d+_\w+")
 _WASSIGN = re.compile(r"^\s*(w\d+_\w+) = ")
+_CBVAR = re.compile(r"\bcb_\w+")
 
 
 @dataclasses.dataclass
@@ -127,7 +128,9 @@ class ColumnGen:
         if self.lblock not in (1, 2, 4):
             raise ValueError(f"tile_lblock must be 1, 2 or 4, got {self.lblock}")
         self.pmask = "1" if self.lblock == 1 else str(2 * self.lblock - 1)
+        self._by_cap = 16
         if self.tile:
+            self._fit_tile_lds()
             bx, by = self._block()
             if bx - ilo - ihi < 8 or by - jlo - jhi < 1:
                 raise UnsupportedStencil(f"IJ extent {self.ext} too wide for a {bx}x{by} tile")
@@ -142,6 +145,26 @@ class ColumnGen:
     def _mem(self, name):
         return name in self.api or name in self.scratch
 
+    def tile_lds_bytes(self) -> int:
+        """Tile mode: the block's static LDS, one plane per shared field and buffer
+        (2 x ``lblock`` buffers of ``by`` x ``bx`` cells)."""
+        bx, by = self._block()
+        return sum(2 * self.lblock * by * bx * self.st.decl(n).dtype.itemsize for n in self.lds)
+
+    def _fit_tile_lds(self) -> None:
+        """Keep the tile's LDS planes within the CU's 160 KB: fewer levels per
+        barrier first, then 8-row blocks when the rows are the automatic choice; a sweep that
+        still does not fit goes to the staged lowering (UnsupportedStencil)."""
+        if self.tile_lds_bytes() <= LDS_BYTES:
+            return
+        if self.lblock > 1:
+            self.lblock, self.pmask = 1, "1"
+        if self.tile_lds_bytes() > LDS_BYTES and int(self.opts.get("tile_by", TILE_BY)) == -1:
+            self._by_cap = 8
+        if self.tile_lds_bytes() > LDS_BYTES:
+            raise UnsupportedStencil(
+                f"tile kernel needs {self.tile_lds_bytes()} B of LDS planes for {sorted(self.lds)} (limit {LDS_BYTES})")
+
     def _block(self) -> Tuple[int, int]:
         """Threads per block in I and J (option ``col_bx``: I width, 256 threads in total; tile
         mode: ``tile_bx`` x ``tile_by`` threads, halo included; defaults 64 x 8 for 8-byte cells,
@@ -149,7 +172,7 @@ class ColumnGen:
         if getattr(self.kernel, "tile", False):
             by = int(self.opts.get("tile_by", TILE_BY))
             if by == -1:
-                by = 16 if self.ext[2] + self.ext[3] <= 1 and self._tile_item() >= 8 else 8
+                by = 16 if self.ext[2] + self.ext[3] <= 1 and self._tile_item() >= 8 and self._by_cap >= 16 else 8
             # two waves per row for cells of 4 bytes or less (a row of 448 B of outputs, r03l sweep)
             bx = int(self.opts.get("tile_bx", 0)) or (128 if self._tile_item() <= 4 and by <= 8 else 64)
             if by not in (4, 8, 16) or bx not in (64, 128) or bx * by > 1024:
@@ -448,11 +471,23 @@ class ColumnGen:
             B.append("const int q = nb >> 3, r = nb & 7, xcd = b & 7, slot = b >> 3;")
             B.append("const int w = (xcd < r) ? xcd * (q + 1) + slot : r * (q + 1) + (xcd - r) * q + slot;")
             B.append("const int tx = (int)threadIdx.x, ty = (int)threadIdx.y;")
-            if TI + eilo + eihi < bx:
-                B.append(f"const int i = (w % nbx) * {TI} + (tx < {TI + eilo + eihi} ? tx : {TI + eilo + eihi - 1}) - {eilo};")
+            # tile order within an XCD's range (option ``tile_order``): 0 I-fast (neighbours in I are
+            # consecutive work items), 1 J-fast, 2 pairs of J rows I-fast (tiles (ti, 2q) and (ti, 2q+1)
+            # consecutive, so both sides of a J halo row run together)
+            torder = int(self.opts.get("tile_order", 0))
+            if torder == 1:
+                B.append("const int nby = (int)gridDim.y, tti = w / nby, ttj = w % nby;")
+            elif torder == 2:
+                B.append("const int nby = (int)gridDim.y, pr = w / (2 * nbx), rem = w % (2 * nbx);")
+                B.append("const bool pair = 2 * pr + 1 < nby;  // the last row of an odd count runs alone")
+                B.append("const int tti = pair ? (rem >> 1) : rem, ttj = pair ? 2 * pr + (rem & 1) : 2 * pr;")
             else:
-                B.append(f"const int i = (w % nbx) * {TI} + tx - {eilo};")
-            B.append(f"const int j = (w / nbx) * {TJ} + ty - {ejlo};")
+                B.append("const int tti = w % nbx, ttj = w / nbx;")
+            if TI + eilo + eihi < bx:
+                B.append(f"const int i = tti * {TI} + (tx < {TI + eilo + eihi} ? tx : {TI + eilo + eihi - 1}) - {eilo};")
+            else:
+                B.append(f"const int i = tti * {TI} + tx - {eilo};")
+            B.append(f"const int j = ttj * {TJ} + ty - {ejlo};")
             B.append(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};")
             B.append(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && ty < {ejlo + TJ} && "
                      f"i < p.ni && j < p.nj;")
@@ -572,11 +607,17 @@ class ColumnGen:
         H.append("}")
         return "\n".join(L), "\n".join(H)
 
+    def _base_fields(self) -> Dict[str, str]:
+        """Column base pointer variable -> the field it addresses."""
+        return {v: key[0] for key, v in self.bases.items()}
+
     @staticmethod
-    def _blockable(levels: List[List[str]], shift: List[str]) -> bool:
+    def _blockable(levels: List[List[str]], shift: List[str], base_fields: Optional[Dict[str, str]] = None) -> bool:
         """Can a level's statements after its LDS barrier wait until the next level's statements
-        before it have run? Exactly one barrier per level, no plane written after it, and no
-        window value assigned after it that the next level's shift or statements read."""
+        before it have run? Exactly one barrier per level, no plane written after it, no window
+        value assigned after it that the next level's shift or statements read, and no field
+        stored to memory after it that the next level's shift or statements load (the caller also
+        refuses loops with run-time K offsets, whose memory reads this text test cannot place)."""
         st = levels[0]
         bars = [q for q, x in enumerate(st) if x.startswith("gtmi::lds_barrier();")]
         if len(bars) != 1:
@@ -586,7 +627,14 @@ class ColumnGen:
             return False
         assigned = {m.group(1) for x in post for m in [_WASSIGN.match(x)] if m}
         later = "\n".join(shift + levels[1][:bars[0]])
-        return not any(re.search(r"\b" + re.escape(n) + r"\b", later) for n in assigned)
+        if any(re.search(r"\b" + re.escape(n) + r"\b", later) for n in assigned):
+            return False
+        if base_fields:
+            stored = {base_fields[v] for x in post if "sstore<" in x for v in _CBVAR.findall(x) if v in base_fields}
+            loaded = {base_fields[v] for v in _CBVAR.findall(later) if v in base_fields}
+            if stored & loaded:
+                return False
+        return True
 
     def _base(self, name, di, dj, out: List[str], writable: bool) -> str:
         key = (name, di, dj)
@@ -947,8 +995,9 @@ class ColumnGen:
                 else:
                     o.append("        int kb = se - 2;")
                     o.append(f"        for (; kb - {R - 1} >= ss; kb -= {R}) {{")
-                blocked = self.lblock > 1 and R % self.lblock == 0 and \
-                    self._blockable([statements() for _ in range(2)], shift_and_fronts(1 % R, mode))
+                blocked = self.lblock > 1 and R % self.lblock == 0 and not direct and \
+                    self._blockable([statements() for _ in range(2)], shift_and_fronts(1 % R, mode),
+                                    self._base_fields())
                 self._blocked_any |= blocked
                 for g in range(0, R, self.lblock if blocked else 1):
                     if not blocked:

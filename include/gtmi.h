@@ -86,7 +86,16 @@ int gtmi_stencil_run(const int64_t* domain, const gtmi_field* fields, int32_t n_
 int gtmi_stencil_run_jsplit(const int64_t* domain, int64_t j_split, int64_t j_skip, const gtmi_field* fields,
                             int32_t n_fields, const gtmi_scalar* scalars, int32_t n_scalars, void* stream);
 
-/* JSON description: {"abi":1,"fields":[...],"scratch":[...],"scalars":[...],"kernels":[...]} */
+/* JSON self-description of the library (codegen/hip.py emits it):
+ *   {"abi": 3,
+ *    "fields":  [{"name", "dtype", "axes": ["I","J","K"], "data_dims": [...]}, ...]   API fields, in
+ *               the order of the gtmi_field array gtmi_stencil_run takes,
+ *    "scratch": [{"name", "dtype", "extent": [[i_lo,i_hi],[j_lo,j_hi]], "axes"}, ...] temporaries
+ *               the caller allocates (domain + extent) and passes after the API fields,
+ *    "scalars": [{"name", "dtype", "used": bool}, ...]                                  in the order of
+ *               the gtmi_scalar array,
+ *    "kernels": ["PlaneKernel" | "ColumnKernel", ...]}                                   launches, in order.
+ * "abi" equals GTMI_ABI_VERSION. */
 const char* gtmi_stencil_signature(void);
 
 /* Message of the last failing gtmi_stencil_run on this thread ("" if none). */

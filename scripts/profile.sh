@@ -19,7 +19,7 @@ for cfg in ${CONFIGS:-hdiff}; do
   cat $OUT/bench_$cfg.json
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg: pmc $c"
-    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${cfg}_$c -o pmc -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-extra > $OUT/pmc_${cfg}_$c.log 2>&1 || exit $?
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${cfg}_$c -o pmc -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --no-extra --placement-candidates 0 --sustain 0 > $OUT/pmc_${cfg}_$c.log 2>&1 || exit $?
   done
 done
 find $OUT -name "*.csv" | head -50

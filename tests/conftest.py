@@ -38,11 +38,25 @@ if os.environ.get("GTMI_PREBUILD_TESTS"):
     def pytest_runtest_makereport(item, call):
         outcome = yield
         rep = outcome.get_result()
-        if _REPORT and rep.when == "call":
+        # the call's outcome, or a set-up that did not pass (a fixture touching the device first:
+        # the test body, and the stencils it constructs, never ran)
+        if _REPORT and (rep.when == "call" or (rep.when == "setup" and not rep.passed)):
             import json
 
             err = None
             if call.excinfo is not None:
                 err = [call.excinfo.type.__name__, str(call.excinfo.value).splitlines()[0][:300] if str(call.excinfo.value) else ""]
             with open(_REPORT, "a") as f:
-                f.write(json.dumps({"test": item.nodeid, "outcome": rep.outcome, "error": err}) + "\n")
+                f.write(json.dumps({"test": item.nodeid, "when": rep.when, "outcome": rep.outcome, "error": err}) + "\n")
+
+    def pytest_collection_modifyitems(session, config, items):
+        """The gpu-marked tests collected (tests/test_prebuild.py checks each has a record)."""
+        if not _REPORT:
+            return
+        import json
+
+        ids = sorted(it.nodeid for it in items if it.get_closest_marker("gpu") is not None)
+        tmp = f"{_REPORT}.collected.{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(ids, f)
+        os.replace(tmp, _REPORT + ".collected")

@@ -2339,6 +2339,33 @@ def _tile_cases():
 _tile_cases()
 
 
+def tile_kwrite_raw(a: F64, out: F64):
+    """A tile sweep whose API output, stored after the LDS barrier one level ahead
+    (``out[0, 0, 1]``, a K-offset write: the field bypasses the register window), is read back at
+    the next level by the statements before the barrier (``c``). Levels blocked two or four to a
+    barrier would run that read before the store and see stale memory, so such a loop keeps one
+    level per barrier (codegen/column.py ``_blockable``). The reference numpy backend
+    runs the K loop outside the horizontal blocks, as the compiled backends do (its debug backend
+    runs each horizontal block over all levels first, so the two disagree on such a program; the
+    fixture comes from the numpy backend)."""
+    with computation(FORWARD):
+        with interval(0, -1):
+            c = out
+            t1 = a * 0.5 + 1.0
+            out[0, 0, 1] = 0.25 * c + t1[1, 0, 0] + t1[0, 1, 0] - t1[0, -1, 0]
+
+
+def _tile_raw_cases():
+    for tag, (ni, nj, nk) in TILE_DOMAINS.items():
+        name = f"tile_kwrite_raw_{tag}"
+        case(name, fields={"a": fs(ni + 1, nj + 2, nk, init=("u", 0.5, 2.0)), "out": fs(ni, nj, nk, init=("u", -1.0, 1.0))},
+             origin={"a": (0, 1, 0), "out": (0, 0, 0)}, domain=(ni, nj, nk), features=("tile",))(tile_kwrite_raw)
+        TILE_GOLDEN.append(name)
+
+
+_tile_raw_cases()
+
+
 # --------------------------------------------------------------------------------------
 # Differential-fuzz programs that take the tile path (tests/fuzz_stencils.py seeds; their
 # sources are committed in tests/fuzz_golden_programs.py so the reference frontend can read

@@ -73,6 +73,13 @@ def test_bench_launcher_dry_run(gpus, decomp):
         assert lp["min_GBps_per_link"] > 0
     else:
         assert "dist" not in rec
+        # C2 and C4 carry their own cpu_ifirst-equivalent figure (BASELINE configs[1])
+        for cfg in ("lap5", "tridiag"):
+            cb = rec["extra_configs"][cfg]["cpu_baseline"]
+            assert "error" not in cb, cb
+            assert cb["value"] > 0 and cb["unit"] == "Mcells/s" and cb["ms_per_call"] > 0
+            assert cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
+            assert cb["dry_run_domain"] == [64, 32, 8]
     for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "roofline", "config"):
         assert key in rec
 

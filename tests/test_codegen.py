@@ -95,7 +95,17 @@ def test_library_loads_and_describes_itself(name):
     assert [s["name"] for s in sig["scalars"]] == list(stencil.parameter_info.keys())
     assert lib.last_error() == ""
     with open(HEADER) as fh:
-        assert f"#define GTMI_ABI_VERSION {ffi.GTMI_ABI_VERSION}" in fh.read()
+        hdr = fh.read()
+    assert f"#define GTMI_ABI_VERSION {ffi.GTMI_ABI_VERSION}" in hdr
+    # the header documents the signature the libraries emit: its version and its keys
+    doc = hdr[hdr.index("JSON self-description"):hdr.index("gtmi_stencil_signature(void)")]
+    assert f'{{"abi": {sig["abi"]},' in doc
+    for key in sig:
+        assert f'"{key}"' in doc, key
+    for group in ("fields", "scratch", "scalars"):
+        for entry in sig[group]:
+            for key in entry:
+                assert f'"{key}"' in doc, (group, key)
 
 
 def test_halo_library_exports_its_header():

@@ -87,6 +87,77 @@ def test_tile_rows_auto_rule(name, block):
     assert _stencil(name, "gt:mi355x", tile_by=8)._gt_run_impl_.compiled.source.count("dim3(64, 16)") == 0
 
 
+def tile_many_planes(a: F64, out: F64):
+    """Six temporaries read across columns: six LDS planes per level (column.py
+    ``_fit_tile_lds``)."""
+    with computation(FORWARD), interval(...):
+        t0 = a * 1.5
+        t1 = a * 2.5 + 1.0
+        t2 = a - 0.5
+        t3 = a * a
+        t4 = a + 2.0
+        t5 = a * 0.25
+        out = t0[1, 0, 0] + t1[0, 1, 0] - t2[1, 0, 0] + t3[0, 1, 0] * t4[1, 0, 0] - t5[1, 0, 0] + t5
+
+
+def tile_eleven_planes(a: F64, out: F64):
+    with computation(FORWARD), interval(...):
+        t0 = a * 1.5
+        t1 = a * 2.5
+        t2 = a - 0.5
+        t3 = a * a
+        t4 = a + 2.0
+        t5 = a * 0.25
+        t6 = a + 3.0
+        t7 = a * 4.0
+        t8 = a - 5.0
+        t9 = a * 6.0
+        t10 = a + 7.0
+        out = (t0[1, 0, 0] + t1[1, 0, 0] + t2[1, 0, 0] + t3[1, 0, 0] + t4[1, 0, 0] + t5[1, 0, 0]
+               + t6[0, 1, 0] + t7[0, 1, 0] + t8[0, 1, 0] + t9[0, 1, 0] + t10[0, 1, 0])
+
+
+def _gen(defn, **opts):
+    st = gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"tile.{defn.__name__}", **opts)
+    return st._gt_run_impl_.compiled
+
+
+def _lds_planes(src):
+    import re
+
+    return [tuple(int(x) for x in m) for m in re.findall(r"__shared__ double lds_\w+\[(\d+)\]\[(\d+)\]\[(\d+)\]", src)]
+
+
+def test_tile_lds_planes_fit_the_cu():
+    """The tile kernel's LDS planes stay within 160 KB: six f64 planes on 16-row
+    blocks need 192 KB at two levels per barrier, so the kernel drops to one level per barrier
+    (96 KB); eleven planes also drop to 8-row blocks when the rows are the automatic choice, and
+    go to the staged lowering when 16 rows are asked for explicitly."""
+    c = _gen(tile_many_planes)
+    planes = _lds_planes(c.source)
+    assert len(planes) == 6 and all(p == (2, 16, 64) for p in planes), planes
+    assert sum(8 * a * b * d for a, b, d in planes) <= 160 * 1024
+    c = _gen(tile_many_planes, tile_lblock=4)
+    assert all(p == (2, 16, 64) for p in _lds_planes(c.source))
+    c = _gen(tile_eleven_planes)
+    planes = _lds_planes(c.source)
+    assert len(planes) == 11 and all(p == (2, 8, 64) for p in planes), planes
+    c = _gen(tile_eleven_planes, tile_by=16)
+    assert not any(getattr(k, "tile", False) for k in c.plan.kernels), c.plan
+    assert c.plan.scratch  # the staged lowering's phases
+
+
+def test_tile_levels_blocked_only_without_memory_raw():
+    """A loop whose API output, stored after the barrier one level ahead, is read back before the
+    next level's barrier keeps one level per barrier; the other tile programs are blocked
+    (golden ``tile_kwrite_raw_*`` runs it under every geometry)."""
+    import stencil_cases as sc
+
+    for lb in (2, 4):
+        assert "one LDS barrier" not in _gen(sc.tile_kwrite_raw, tile_lblock=lb).source
+        assert "one LDS barrier" in _gen(fwd_recurrence_ij_temp, tile_lblock=lb).source
+
+
 def test_tile_off_uses_staged_lowering():
     st = _stencil("fwd_recurrence_ij_temp", "gt:mi355x", tile=0)
     plan = st._gt_run_impl_.compiled.plan
@@ -198,3 +269,27 @@ def test_tile_vs_numpy_backend(name, geom):
     st(**dev, origin=origins, domain=domain)
     got = storage.to_numpy(dev["out"])
     np.testing.assert_array_equal(got, ref["out"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defn", [tile_many_planes, tile_eleven_planes])
+def test_tile_many_planes_vs_numpy_backend(defn):
+    """The LDS-budget fallbacks (one level per barrier, 8-row blocks) against the numpy backend
+    on a ragged domain."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from gt4py_amd import storage
+
+    ni, nj, nk = 131, 23, 13
+    rng = np.random.default_rng(11)
+    arrays = {"a": rng.uniform(0.5, 2.0, (ni + 1, nj + 1, nk)), "out": np.zeros((ni, nj, nk))}
+    origins = {"a": (0, 0, 0), "out": (0, 0, 0)}
+    ref = {k: v.copy() for k, v in arrays.items()}
+    gtscript.stencil(backend="numpy", definition=defn, name=f"tile.np.{defn.__name__}")(
+        **ref, origin=origins, domain=(ni, nj, nk))
+    st = gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"tile.{defn.__name__}")
+    dev = {k: storage.from_array(v, v.dtype, backend="gt:mi355x", aligned_index=origins[k]) for k, v in arrays.items()}
+    st(**dev, origin=origins, domain=(ni, nj, nk))
+    np.testing.assert_array_equal(storage.to_numpy(dev["out"]), ref["out"])
