@@ -129,6 +129,7 @@ class Mi355xBackend(BaseBackend):
         "tile_bx": {"versioning": True, "type": int, "description": "tile kernels: I lanes per block (64 or 128)"},
         "tile_order": {"versioning": True, "type": int, "description": "tile kernels: work order of the tiles within an XCD's range (0 I-fast, default; 1 J-fast; 2 pairs of J rows, I-fast)"},
         "tile_ti": {"versioning": True, "type": int, "description": "tile kernels: output columns per tile in I (default: 64 minus the sweep's I extent)"},
+        "exact_fma": {"versioning": True, "type": int, "description": "f64 add/sub of an exact product (power-of-two literal x a value widened from f32 or a <= 32-bit int) as one fma: bit-identical, one instruction fewer (1, default)"},
         "verbose": {"versioning": False, "type": bool, "description": "print the hipcc command"},
         "oir_pipeline": {"versioning": True, "type": object, "description": "accepted for compatibility"},
     }

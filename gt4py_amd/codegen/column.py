@@ -848,6 +848,7 @@ class ColumnGen:
                 return wvar(acc.name, di, dj, dk)
 
             rend = ExprRenderer(resolve, lambda n: f"s_{cname(n)}", lambda ax: ["i", "j", "k"][ax])
+            rend.exact_fma = bool(int(self.opts.get("exact_fma", 1)))
             self._kaddr = kaddr
 
             def shift_and_fronts(slot: Optional[int], mode: str, reg_u: Optional[int] = None,

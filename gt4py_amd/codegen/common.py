@@ -80,13 +80,67 @@ _MATH1 = {
 }
 
 
+def _exactly_widened(e) -> bool:
+    """``e`` is an f64 value cast from a type whose every value, times a power of two of modest
+    exponent, is exact in f64 (f32, integers of at most 32 bits)."""
+    if not isinstance(e, ir.Cast) or e.dtype != DataType.FLOAT64:
+        return False
+    src = getattr(e.expr, "dtype", None)
+    return src in (DataType.FLOAT32, DataType.INT8, DataType.INT16, DataType.INT32)
+
+
+def _pow2_literal(e):
+    """The value of an f64 power-of-two literal (possibly behind casts) with |exponent| <= 64."""
+    while isinstance(e, ir.Cast):
+        e = e.expr
+    if not isinstance(e, ir.Literal) or e.dtype == DataType.BOOL:
+        return None
+    try:
+        v = float(e.value)
+    except (TypeError, ValueError):
+        return None
+    if v == 0.0 or not math.isfinite(v):
+        return None
+    m, x = math.frexp(abs(v))
+    return v if (m == 0.5 and -64 <= x <= 64) else None
+
+
 class ExprRenderer:
-    """Renders typed IR expressions to C++; ``resolve(FieldAccess) -> str`` is supplied."""
+    """Renders typed IR expressions to C++; ``resolve(FieldAccess) -> str`` is supplied.
+
+    ``exact_fma``: an f64 ``p +- c`` / ``c - p`` whose product ``p`` = power-of-two literal x value
+    widened from f32 (or a <= 32-bit integer) is rendered as one ``fma``. The product is exact, so
+    the single rounding of the fma equals the rounding of the separate add: bit-identical results,
+    one instruction fewer (the f32 hdiff cast tree's ``4.0 * f64(u) - f64(sum)``)."""
+
+    exact_fma = True
 
     def __init__(self, resolve, scalar_name, axis_index=None):
         self.resolve = resolve
         self.scalar_name = scalar_name
         self.axis_index = axis_index
+
+    def _exact_product(self, e):
+        """(literal C text, other factor C text) when ``e`` is such an exact f64 product."""
+        if not (self.exact_fma and isinstance(e, ir.BinaryOp) and e.op == "*" and e.dtype == DataType.FLOAT64):
+            return None
+        for lit, other in ((e.left, e.right), (e.right, e.left)):
+            v = _pow2_literal(lit)
+            if v is not None and _exactly_widened(other):
+                return v, self.r(other)
+        return None
+
+    def _fma(self, e):
+        if e.op not in ("+", "-") or e.dtype != DataType.FLOAT64:
+            return None
+        lp, rp = self._exact_product(e.left), self._exact_product(e.right)
+        if lp is not None:  # p + c, p - c
+            c = self.r(e.right)
+            return f"__builtin_fma({literal(lp[0], DataType.FLOAT64)}, {lp[1]}, {c if e.op == '+' else f'(-{c})'})"
+        if rp is not None:  # c + p, c - p
+            v = rp[0] if e.op == "+" else -rp[0]
+            return f"__builtin_fma({literal(v, DataType.FLOAT64)}, {rp[1]}, {self.r(e.left)})"
+        return None
 
     def __call__(self, e: ir.Expr) -> str:
         return self.r(e)
@@ -101,6 +155,9 @@ class ExprRenderer:
         if isinstance(e, ir.Cast):
             return f"(({e.dtype.ctype})({self.r(e.expr)}))"
         if isinstance(e, ir.BinaryOp):
+            f = self._fma(e)
+            if f is not None:
+                return f
             a, b = self.r(e.left), self.r(e.right)
             if e.op in ("and", "or"):
                 return f"({a} {'&&' if e.op == 'and' else '||'} {b})"

@@ -912,6 +912,7 @@ class PlaneGen:
                 return f"{ref.val.c}_{slot}_{r}"
 
             rend = _VRenderer(resolve, lambda n: f"s_{cname(n)}", self._axis_index(lead, e))
+            rend.exact_fma = bool(int(self.opts.get("exact_fma", 1)))
             if V > 1:
                 out.append(f"// element {e}")
             for s in code:

@@ -226,6 +226,13 @@ class HaloStencil:
         # (+2.0-2.1 % vs +2.2-2.7 % per step)
         self.unpack_on_main = bands_on_halo is None and bands == "unpack_main"
         self.fuse_strips = os.environ.get("GTMI_HALO_STRIPS", "fused") == "fused"
+        # gate (``GTMI_HALO_GATE=1``): the interior waits for the pack, so RCCL's kernel and the
+        # interior become ready together and RCCL's high-priority queue is dispatched first --
+        # otherwise the interior's workgroups fill every CU and RCCL's kernel runs at the
+        # interior's tail. With the strips on the halo stream they then run as
+        # soon as the transfer lands, beside the interior, when the stencil has no scratch
+        # temporaries the two launches would share.
+        self.gate = os.environ.get("GTMI_HALO_GATE", "0") == "1"
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}
@@ -261,6 +268,8 @@ class HaloStencil:
             self._stream.wait_event(ready)
             with torch.cuda.stream(self._stream):
                 works = self.exchange.start(fields)
+            if self.gate:
+                main.wait_event(self._stream.record_event())
             # the transfers are posted before the interior is enqueued; with split > 1 the interior
             # runs as that many row bands, so CU slots free up between launches
             rows = nj - 2 * h
@@ -277,9 +286,10 @@ class HaloStencil:
                 self.exchange.finish(works)
                 if self.bands_on_halo:
                     # the two boundary strips follow the unpack on the halo stream (they write rows
-                    # the interior does not) -- but only after the interior: both may use the
+                    # the interior does not) -- but only after the interior when both may use the
                     # launcher's per-domain scratch buffers (a band as tall as the interior)
-                    self._stream.wait_event(interior_done)
+                    if not (self.gate and not _uses_scratch(self.stencil)):
+                        self._stream.wait_event(interior_done)
                     self._strips(kw, origin, ni, nj, nk)
             main.wait_stream(self._stream)
             if self.bands_on_halo:
@@ -303,6 +313,14 @@ class HaloStencil:
             return
         self.stencil(**kw, origin=origin, domain=(ni, h, nk), validate_args=False)
         self.stencil(**kw, origin=self._shifted(origin, nj - h), domain=(ni, h, nk), validate_args=False)
+
+
+def _uses_scratch(stencil) -> bool:
+    """Does the stencil's library allocate scratch temporaries (shared by concurrent calls)?
+    Unknown backends count as yes."""
+    compiled = getattr(getattr(stencil, "_gt_run_impl_", None), "compiled", None)
+    plan = getattr(compiled, "plan", None)
+    return plan is None or bool(plan.scratch)
 
 
 def halo_fields_read_only(stencil, names) -> bool:

@@ -26,6 +26,19 @@ if os.environ.get("GTMI_PREBUILD_TESTS"):
 
     torch.cuda.is_available = lambda: True
     _gt_storage._device_of = lambda info: "cpu"  # tests that allocate first reach their stencils
+    # the full-size tests allocate GBs per field on the host stand-in; eight workers at once ran
+    # the container out of memory (a worker was killed, its test left unrecorded). A stencil is
+    # built before its fields, so stop such a test at its first large allocation instead
+    _gt_empty = _gt_storage.empty
+
+    def _bounded_empty(shape, *args, **kwargs):
+        import numpy as _np
+
+        if int(_np.prod(shape)) > (64 << 20):
+            raise MemoryError("GTMI_PREBUILD_TESTS: full-size field not allocated on the host stand-in")
+        return _gt_empty(shape, *args, **kwargs)
+
+    _gt_storage.empty = _bounded_empty
 
     def _no_launch(self, *args, **kwargs):
         raise RuntimeError("GTMI_PREBUILD_TESTS: built, not launched")

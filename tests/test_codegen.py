@@ -172,3 +172,36 @@ def test_sweep_cache_end_auto_rule():
     assert "if (ks < rbase) ks = rbase;" in srcs["tridiag"]
     assert "const int tc1 = nk - rbase, tc0 = tc1 - tlen;" in srcs["vadv"]
     assert "the reader's band: prefetched here" in srcs["vadv"] and "the reader's band" not in srcs["tridiag"]
+
+
+def test_exact_products_render_as_fma():
+    """An f64 add/sub of power-of-two literal x value widened from f32 renders as one fma (the
+    product is exact, so one rounding equals the separate add's): the f32 hdiff cast tree's
+    ``4.0 * f64(u) - f64(sum)``. f64 operands (the product may overflow) and other literals keep
+    the separate multiply; ``exact_fma=0`` turns it off. Bit-exactness on the GPU: the f32 hdiff
+    and mixed-precision goldens and the full-size C5 tile vs the C oracle (test_gpu_parity.py)."""
+    from gt4py_amd.codegen.common import ExprRenderer
+    from gt4py_amd.ir import BinaryOp, Cast, DataType, Literal, ScalarAccess
+
+    f32 = ScalarAccess("u", DataType.FLOAT32)
+    f64 = ScalarAccess("v", DataType.FLOAT64)
+    wide = Cast(DataType.FLOAT64, f32)
+    rend = ExprRenderer(lambda a: "?", lambda n: n)
+
+    def expr(lit, x, op, c):
+        p = BinaryOp("*", Literal(lit, DataType.FLOAT64), x, DataType.FLOAT64)
+        return BinaryOp(op, p, c, DataType.FLOAT64)
+
+    assert rend(expr(4.0, wide, "-", f64)).startswith("__builtin_fma(")
+    assert rend(BinaryOp("-", f64, BinaryOp("*", wide, Literal(0.25, DataType.FLOAT64), DataType.FLOAT64),
+                         DataType.FLOAT64)).startswith("__builtin_fma(((double)(-0x1")
+    assert "__builtin_fma" not in rend(expr(4.0, f64, "-", f64))  # f64 factor: 4x may overflow
+    assert "__builtin_fma" not in rend(expr(3.0, wide, "+", f64))  # not a power of two
+    rend.exact_fma = False
+    assert "__builtin_fma" not in rend(expr(4.0, wide, "-", f64))
+    c = sc.CASES["hdiff_f32"]
+    src = gtscript.stencil(backend="gt:mi355x", definition=c.definition, name="gpu.hdiff_f32")._gt_run_impl_.compiled.source
+    assert "__builtin_fma" in src
+    c = sc.CASES["hdiff_f64"]
+    src = gtscript.stencil(backend="gt:mi355x", definition=c.definition, name="gpu.hdiff_f64")._gt_run_impl_.compiled.source
+    assert "__builtin_fma" not in src

@@ -298,3 +298,19 @@ def test_overlap_off_when_a_halo_field_is_written():
     dec = Decomposition2D(16, 16, 2, 1)
     assert HaloStencil2D(st, ["a"], dec, 0, (1, 1)).overlap
     assert not HaloStencil2D(st, ["b"], dec, 0, (1, 1)).overlap
+
+
+def test_gated_strips_run_beside_the_interior_only_without_scratch():
+    """GTMI_HALO_GATE: the boundary strips may skip waiting for the interior only when the two
+    launches share no scratch temporaries (gt:mi355x plans say; other backends count as sharing)."""
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import stencil_cases as sc
+
+    from gt4py_amd import gtscript
+    from gt4py_amd.distributed.halo import _uses_scratch
+
+    assert not _uses_scratch(gtscript.stencil(backend="gt:mi355x", definition=sc.hdiff_f64, name="dist.gate.hdiff"))
+    assert _uses_scratch(gtscript.stencil(backend="gt:mi355x", definition=sc.staged_forward_ij_temp,
+                                          name="dist.gate.staged", tile=0))
+    assert _uses_scratch(gtscript.stencil(backend="numpy", definition=sc.hdiff_f64, name="dist.gate.np"))

@@ -71,7 +71,7 @@ def _oracle_hdiff(core, coeff, h, wrap_i):
 
 
 @pytest.mark.parametrize("stream_mode", ["main", "main_bands", "side", "side_bands_main", "side_unpack_main", "side_split3",
-                                         "diag"])
+                                         "diag", "side_gate", "side_gate_unpack_main"])
 @pytest.mark.parametrize("mode", ["jstrips", "tiles2d", "tiles2d_jperiodic"])
 def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     import torch
@@ -88,6 +88,8 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
     out = storage.zeros((ni, nj, nk), np.float64, backend="gt:mi355x")
     wrap_i = mode == "tiles2d"
     origin = {"in_field": (h, h, 0), "out_field": (0, 0, 0), "coeff": (0, 0, 0)}
+    if "gate" in stream_mode and mode != "jstrips":
+        pytest.skip("the gated interior (GTMI_HALO_GATE) is a J-strip option")
     if mode == "jstrips":
         if stream_mode == "diag":
             pytest.skip("the diagonal (one-phase) scheme is a 2-D tile exchange")
@@ -98,6 +100,8 @@ def test_rccl_halo_hdiff_vs_c_oracle(rccl_group, mode, stream_mode):
         run = HaloStencil2D(st, ["in_field"], dec, 0, (h, h), force_comm=True,
                             scheme="diagonal" if stream_mode == "diag" else "two_phase")
     run.stream_mode = {"diag": "main"}.get(stream_mode, stream_mode.split("_")[0])
+    if hasattr(run, "gate"):
+        run.gate = "gate" in stream_mode  # interior waits for the pack; strips beside the interior
     if hasattr(run, "bands_on_halo"):
         run.bands_on_halo = not stream_mode.endswith("bands_main")
         run.split = 3 if stream_mode.endswith("split3") else 1
