@@ -1058,6 +1058,7 @@ def main():
             "plain_ms_per_step": round(float(mine[0]) / args.steps * 1e3, 4),
             "plain_kernel_ms": round(float(mine[1]), 4) if km_p is not None else None,
             "exchange_overhead": round(float(mine[2]), 4),
+            "halo_schedule": wl.halo.schedule() if hasattr(getattr(wl, "halo", None), "schedule") else None,
             "note": "plain = one launch over the whole local tile on the same buffers, no exchange; "
                     "exchange_overhead = halo-path time / plain time - 1 per rank, max over ranks",
         }
@@ -1071,7 +1072,8 @@ def main():
         halo_ab = {"plain_ms_per_step": round(el_p / args.steps * 1e3, 4), "plain_kernel_ms": round(km_p, 4),
                    "halo_host_enqueue_ms_per_step": round(enq / args.steps * 1e3, 4),
                    "halo_ms_per_step": round(min(elapsed, el_h) / args.steps * 1e3, 4),
-                   "overhead": round(min(elapsed, el_h) / el_p - 1.0, 4)}
+                   "overhead": round(min(elapsed, el_h) / el_p - 1.0, 4),
+                   "halo_schedule": wl.halo.schedule() if hasattr(getattr(wl, "halo", None), "schedule") else None}
     ni, nj, nk = wl.domain
     cells_per_step = ni * nj * nk
     total_cells = wl.global_ij[0] * wl.global_ij[1] * nk * args.steps

@@ -219,20 +219,31 @@ class HaloStencil:
         if self.stream_mode not in ("side", "main"):
             raise ValueError(f"stream_mode must be 'side' or 'main', got {self.stream_mode!r}")
         self.split = max(1, int(split if split is not None else os.environ.get("GTMI_HALO_SPLIT", "1")))
-        bands = os.environ.get("GTMI_HALO_BANDS", "unpack_main")
+        # gate (``GTMI_HALO_GATE``: 1, 0, or auto = on when the neighbours are other ranks): the
+        # interior waits for the pack, so RCCL's kernel and the interior become ready together and
+        # RCCL's high-priority queue is dispatched first -- otherwise the interior's workgroups fill
+        # every CU and RCCL's kernel completes only at the interior's tail, which puts the whole
+        # transfer on the critical path. With the gate the unpack and the strips default to the
+        # halo stream and run as soon as the faces land, beside the interior (when the stencil has
+        # no scratch temporaries the two launches would share). One GPU as its own neighbour
+        # (a transfer of ~25 us) measures the gate's hand-offs, not its gain: +3.4 % against +2.5 %
+        # per step (profiles/r06/r06c_halo_gate_*), so auto keeps it off there.
+        gate = os.environ.get("GTMI_HALO_GATE", "auto")
+        self.gate = (world_size > 1 and not force_comm) if gate == "auto" else gate == "1"
+        bands = os.environ.get("GTMI_HALO_BANDS", "halo" if self.gate else "unpack_main")
         self.bands_on_halo = bands_on_halo if bands_on_halo is not None else bands == "halo"
         # "unpack_main" (default): the caller's stream itself waits on RCCL's stream, unpacks and
         # computes the strips -- one cross-queue hand-off after the transfer instead of two
         # (+2.0-2.1 % vs +2.2-2.7 % per step)
         self.unpack_on_main = bands_on_halo is None and bands == "unpack_main"
         self.fuse_strips = os.environ.get("GTMI_HALO_STRIPS", "fused") == "fused"
-        # gate (``GTMI_HALO_GATE=1``): the interior waits for the pack, so RCCL's kernel and the
-        # interior become ready together and RCCL's high-priority queue is dispatched first --
-        # otherwise the interior's workgroups fill every CU and RCCL's kernel runs at the
-        # interior's tail. With the strips on the halo stream they then run as
-        # soon as the transfer lands, beside the interior, when the stencil has no scratch
-        # temporaries the two launches would share.
-        self.gate = os.environ.get("GTMI_HALO_GATE", "0") == "1"
+
+    def schedule(self) -> Dict[str, object]:
+        """The GPU schedule this runner uses (reported in the bench line's ``dist``)."""
+        return {"overlap": self.overlap, "transport": _backend_name(self.exchange.group), "stream": self.stream_mode,
+                "gate": self.gate, "split": self.split,
+                "strips": "halo stream" if self.bands_on_halo else ("caller's stream after the unpack"
+                                                                     if self.unpack_on_main else "caller's stream")}
 
     def _shifted(self, origin: Dict[str, Tuple[int, int, int]], dj: int) -> Dict[str, Tuple[int, int, int]]:
         return {k: (o[0], o[1] + dj, *o[2:]) for k, o in origin.items()}

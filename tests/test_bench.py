@@ -55,6 +55,8 @@ def test_bench_launcher_dry_run(gpus, decomp):
         for k in ("step_ms", "plain_ms_per_step", "plain_kernel_ms", "exchange_overhead"):
             assert k in d
         assert isinstance(d["exchange_overhead"], float)
+        if decomp == "jstrips":  # real peers: the interior is gated on the pack
+            assert d["halo_schedule"]["gate"] is True and d["halo_schedule"]["strips"] == "halo stream"
         assert rec["roofline"]["traffic"] is None and "halo step" in rec["roofline"]["traffic_source"]
         assert "step_ms" in rec["roofline"] and "kernel_ms" not in rec["roofline"]
         # C5 (the f32 tile) through the same N-rank path, whole-job cells/s
@@ -149,3 +151,5 @@ def test_bench_halo_selfcomm_link_probe():
     (r0,) = lp["ranks"]
     assert r0["peers"] == [0] and r0["payload_ok"] and r0["GBps_per_link_each_way"] > 0
     assert rec["halo_ab"]["overhead"] > -0.5
+    # one GPU as its own neighbour keeps the ungated schedule (auto gate: real peers only)
+    assert rec["halo_ab"]["halo_schedule"]["gate"] is False
