@@ -140,6 +140,22 @@ def _make_array(spec: FieldSpec, rng: np.random.Generator) -> np.ndarray:
         arr = np.broadcast_to(base + jit, shape).copy()
     elif isinstance(init, tuple) and init[0] == "const":
         arr = np.full(shape, init[1])
+    elif isinstance(init, tuple) and init[0] == "special":
+        # IEEE edge values among U(lo, hi) ("special", lo, hi[, fraction[, finite only]]): signed
+        # zeros, denormals, the largest finite values and (unless finite only) NaN and infinities
+        # of the field's type, each cell special with probability ``fraction`` (default 1/8)
+        frac = init[3] if len(init) > 3 else 0.125
+        pool = [0.0, -0.0, 1.0, -1.0, 0.5]
+        if dt == np.float32:
+            pool += [1.4e-45, -1.4e-45, 1.1754944e-38, -3.0e-39, 3.4028235e38, -3.4028235e38]
+        else:
+            pool += [5e-324, -5e-324, 2.2250738585072014e-308, 1.7976931348623157e308, -1.7976931348623157e308]
+        if not (len(init) > 4 and init[4]):
+            pool += [np.nan, np.inf, -np.inf]
+        special = rng.random(size=shape) < frac
+        pick = rng.integers(0, len(pool), size=shape)
+        rnd = rng.uniform(init[1], init[2], size=shape)
+        arr = np.where(special, np.asarray(pool)[pick], rnd)
     else:
         raise ValueError(f"unknown init {init!r}")
     arr = np.asarray(arr).astype(dt)
@@ -357,6 +373,47 @@ def _tridiag_fields(ni, nj, nk):
 
 
 case("tridiag", fields=_tridiag_fields(8, 6, 32), features=("hot",))(tridiagonal_solver)
+
+
+# IEEE edge values through the hot path (signed zeros, denormals, the largest finite values -- whose
+# sums overflow -- NaN and infinities, mixed with ordinary values): the f32 cast tree, the limiter's
+# comparisons and the Thomas solve's divisions, against the reference numpy backend
+def _special(*shape, dtype="f8", lo=-10.0, hi=10.0, frac=0.125, finite=False):
+    return fs(*shape, dtype=dtype, init=("special", lo, hi, frac, finite))
+
+
+for _dt, _defn in (("f4", hdiff_f32), ("f8", hdiff_f64)):
+    case(
+        f"hdiff_{'f32' if _dt == 'f4' else 'f64'}_special",
+        fields={
+            "in_field": _special(41, 33, 5, dtype=_dt),
+            "out_field": fs(37, 29, 5, dtype=_dt, init="zeros"),
+            "coeff": _special(37, 29, 5, dtype=_dt, lo=0.0, hi=0.5),
+        },
+        origin=_HD_ORIGIN,
+        domain=(37, 29, 5),
+        features=("hot",),
+    )(_defn)
+case(
+    "lap5_special",
+    fields={"in_field": _special(39, 31, 5), "out_field": fs(37, 29, 5, init="zeros")},
+    origin={"in_field": (1, 1, 0), "out_field": (0, 0, 0)},
+    domain=(37, 29, 5),
+    features=("hot",),
+)(lap5)
+case(
+    "tridiag_special",
+    fields={
+        # finite edge values (a NaN would poison its whole column through both sweeps), a zero
+        # or denormal pivot now and then (infinities and NaN made by the divisions themselves)
+        "inf": _special(9, 7, 12, lo=-1.0, hi=1.0, frac=0.05, finite=True),
+        "diag": _special(9, 7, 12, lo=4.0, hi=5.0, frac=0.03, finite=True),
+        "sup": _special(9, 7, 12, lo=-1.0, hi=1.0, frac=0.05, finite=True),
+        "rhs": _special(9, 7, 12, frac=0.05, finite=True),
+        "out": fs(9, 7, 12, init="zeros"),
+    },
+    features=("hot",),
+)(tridiagonal_solver)
 case("tridiag_k2", fields=_tridiag_fields(5, 4, 2), features=("hot",))(tridiagonal_solver)
 case(
     "tridiag_subdomain",
@@ -1104,6 +1161,28 @@ def mixed_precision(a: F32, b: F64, out32: F32, out64: F64):
         t64 = a * 2.0 + b
         out32 = t32 * a - b
         out64 = t64 / (a + 3) + t32
+
+
+def exact_products(a: F32, b: F64, c: F32, n: Field[np.int32], o1: F64, o2: F64, o3: F32, o4: F64):
+    """f64 adds and subtractions of exact products -- a power-of-two literal times a value widened
+    from f32 or int32 -- which gt:mi355x renders as one fma (codegen/common.py ``exact_fma``), on
+    IEEE edge values: signed zeros, denormals, the largest finite values, NaN and infinities."""
+    with computation(PARALLEL), interval(...):
+        o1 = 4.0 * a - b
+        o2 = b - 0.5 * c
+        o3 = 2.0 * a + c
+        o4 = b + n * 8.0
+
+
+case(
+    "exact_products",
+    fields={"a": fs(11, 7, 6, dtype="f4", init=("special", -3.0, 3.0, 0.5)),
+            "b": fs(11, 7, 6, init=("special", -3.0, 3.0, 0.5)),
+            "c": fs(11, 7, 6, dtype="f4", init=("special", -3.0, 3.0, 0.5)),
+            "n": fs(11, 7, 6, dtype="i4", init=("int", -2**31, 2**31 - 1)),
+            "o1": fs(11, 7, 6, init="zeros"), "o2": fs(11, 7, 6, init="zeros"),
+            "o3": fs(11, 7, 6, dtype="f4", init="zeros"), "o4": fs(11, 7, 6, init="zeros")},
+)(exact_products)
 
 
 case(
