@@ -127,6 +127,7 @@ class Mi355xBackend(BaseBackend):
         "tile_by": {"versioning": True, "type": int, "description": "tile kernels: J rows of threads per block (4, 8, 16; -1 auto, default: 16 for a one-row J halo on 8-byte cells, else 8)"},
         "tile_lblock": {"versioning": True, "type": int, "description": "tile kernels: levels per LDS barrier in the steady-state loop (1, 2, 4)"},
         "tile_bx": {"versioning": True, "type": int, "description": "tile kernels: I lanes per block (64 or 128)"},
+        "tile_rows": {"versioning": True, "type": int, "description": "tile kernels: J rows per thread (1, default; 2: each thread carries two columns, by rows apart, so the block covers 2 x tile_by rows)"},
         "tile_order": {"versioning": True, "type": int, "description": "tile kernels: work order of the tiles within an XCD's range (0 I-fast, default; 1 J-fast; 2 pairs of J rows, I-fast)"},
         "tile_ti": {"versioning": True, "type": int, "description": "tile kernels: output columns per tile in I (default: 64 minus the sweep's I extent)"},
         "exact_fma": {"versioning": True, "type": int, "description": "f64 add/sub of an exact product (power-of-two literal x a value widened from f32 or a <= 32-bit int) as one fma: bit-identical, one instruction fewer (1, default)"},

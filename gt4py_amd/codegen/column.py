@@ -63,6 +63,18 @@ TILE_BY = -1
 # scratch_product -0.8 %, staged -0.6 %, the rest within +-0.4 %; kernels where no loop can be
 # blocked keep two planes and one barrier per level.
 TILE_LBLOCK = 2
+# tile mode: J rows per thread (option ``tile_rows``): 2 makes a block of bx x by threads cover
+# 2 x by rows, each thread carrying the state of two columns (the second one by rows further down,
+# its code the first row's with the per-column names renamed), so 128 x 8 threads can hold a
+# 112 x 15 tile -- the only way past the 1024-thread cap to a tile both wide and tall
+TILE_ROWS = 1
+_ROW1 = re.compile(r"\b(w\d+_\w+|rg\d+_\w+|cb_\w+|sn\d+_\w+|j|ty|alive|own)\b")
+
+
+def _row1(line: str) -> str:
+    """Tile mode, a thread's second row: the same code on its own column state (window, ring and
+    snapshot registers, column bases, j, ty, alive and own renamed)."""
+    return _ROW1.sub(r"\1_r1", line)
 _KVAR = re.compile(r"\bk\b")
 _WVAR = re.compile(r"\bw\d+_\w+")
 _WASSIGN = re.compile(r"^\s*(w\d+_\w+) = ")
@@ -129,9 +141,13 @@ class ColumnGen:
             raise ValueError(f"tile_lblock must be 1, 2 or 4, got {self.lblock}")
         self.pmask = "1" if self.lblock == 1 else str(2 * self.lblock - 1)
         self._by_cap = 16
+        self.trows = int(opts.get("tile_rows", TILE_ROWS)) if self.tile else 1
+        if self.trows not in (1, 2):
+            raise ValueError(f"tile_rows must be 1 or 2, got {self.trows}")
         if self.tile:
             self._fit_tile_lds()
             bx, by = self._block()
+            by *= self.trows
             if bx - ilo - ihi < 8 or by - jlo - jhi < 1:
                 raise UnsupportedStencil(f"IJ extent {self.ext} too wide for a {bx}x{by} tile")
             ti = int(opts.get("tile_ti", 0))
@@ -149,7 +165,7 @@ class ColumnGen:
         """Tile mode: the block's static LDS, one plane per shared field and buffer
         (2 x ``lblock`` buffers of ``by`` x ``bx`` cells)."""
         bx, by = self._block()
-        return sum(2 * self.lblock * by * bx * self.st.decl(n).dtype.itemsize for n in self.lds)
+        return sum(2 * self.lblock * by * self.trows * bx * self.st.decl(n).dtype.itemsize for n in self.lds)
 
     def _fit_tile_lds(self) -> None:
         """Keep the tile's LDS planes within the CU's 160 KB: fewer levels per
@@ -199,7 +215,7 @@ class ColumnGen:
             unit = (128 if item >= 8 else 64) // item
             if ti >= unit:
                 ti -= ti % unit
-        return ti, by - ejlo - ejhi
+        return ti, by * self.trows - ejlo - ejhi
 
     def _tile_item(self) -> int:
         """Largest cell size among the API fields the tile kernel stores (8 if none)."""
@@ -491,9 +507,15 @@ class ColumnGen:
             B.append(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};")
             B.append(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && ty < {ejlo + TJ} && "
                      f"i < p.ni && j < p.nj;")
+            if self.trows == 2:  # the thread's second row, by rows further down the tile
+                B.append(f"const int ty_r1 = ty + {by}, j_r1 = j + {by};")
+                B.append(_row1(f"const bool alive = i < p.ni + {eihi} && j < p.nj + {ejhi};"))
+                B.append(_row1(f"const bool own = tx >= {eilo} && tx < {eilo + TI} && ty >= {ejlo} && "
+                               f"ty < {ejlo + TJ} && i < p.ni && j < p.nj;"))
             for n in sorted(self.lds):
                 ct = self.st.decl(n).dtype.ctype
-                B.append(f"__shared__ {ct} lds_{cname(n)}[{2 * self.lblock}][{by}][{bx}];  // this level's plane (k & {self.pmask})")
+                B.append(f"__shared__ {ct} lds_{cname(n)}[{2 * self.lblock}][{by * self.trows}][{bx}];  "
+                         f"// this level's plane (k & {self.pmask})")
         elif int(self.opts.get("col_order", 1)) == 1:
             # XCD-aware: consecutive column blocks (along I, then J) run on one XCD (8 XCDs, round-robin dispatch)
             B.append("const int nbx = (int)gridDim.x, nb = nbx * (int)gridDim.y;")
@@ -512,6 +534,7 @@ class ColumnGen:
             B.append(f"const {s.dtype.ctype} s_{cname(s.name)} = p.s_{cname(s.name)};")
         # column base pointers: the i/j part of every address, computed once per thread
         self.bases: Dict[Tuple[str, int, int], str] = {}
+        nb0 = len(B)
         for li in self.kernel.loops:
             inf = self.info[li]
             for (name, di, dj) in list(inf.win) + [(n, None, None) for n in sorted(inf.direct)]:
@@ -524,6 +547,8 @@ class ColumnGen:
                 for acc, w in iter_accesses(sec.body):
                     if isinstance(acc, ir.FieldAccess) and acc.name in inf.direct:
                         self._base(acc.name, acc.offset[0], acc.offset[1], B, acc.name in written)
+        if self.trows == 2:
+            B += [_row1(x) for x in B[nb0:]]
         if self.tail is not None:
             t = self.tail
             B.append(f"extern __shared__ __attribute__((aligned(16))) char gtmi_lds[];")
@@ -713,11 +738,36 @@ class ColumnGen:
 
         P = self.ring
         step = "+" if fwd else "-"
+
+        def dup(code: List[str]) -> List[str]:
+            """Per-column code for every row of the thread (tile_rows)."""
+            return code + [_row1(x) for x in code] if self.trows == 2 else code
+
+        def merged(stmts: List[str]) -> List[str]:
+            """A level's statements for every row of the thread, interleaved between the LDS
+            barriers (both rows' planes are written before any row reads across columns); the
+            level's ``k_next`` update (stmts[0]) once."""
+            if self.trows == 1:
+                return stmts
+            chunks, cur = [], []
+            for x in stmts[1:]:
+                if x.startswith("gtmi::lds_barrier();"):
+                    chunks.append((cur, x))
+                    cur = []
+                else:
+                    cur.append(x)
+            res = stmts[:1]
+            for c, bar in chunks:
+                res += c + [_row1(x) for x in c] + [bar]
+            return res + cur + [_row1(x) for x in cur]
+
         out = [f"{{  // vertical loop {li} ({order.name})"]
+        decls = []
         for (name, di, dj), rng in win.items():
             t = decl_dtype[name].ctype
             for d in range(rng[0], rng[1] + 1):
-                out.append(f"    {t} {wvar(name, di, dj, d)} = ({t})0;")
+                decls.append(f"    {t} {wvar(name, di, dj, d)} = ({t})0;")
+        out += dup(decls)
         out.append("    int k_next = -0x7fffffff;")
         front = {}
         for key, rng in win.items():
@@ -939,9 +989,9 @@ class ColumnGen:
             def entry_level(slot, mode) -> List[str]:
                 """A segment's first level, which may follow a gap: full window reload unless it
                 continues the sweep (the only level with loads inside a branch)."""
-                return (["if (k != k_next) {  // (re)load the full K-window"] + ["    " + x for x in reload()]
-                        + ["} else {"] + ["    " + x for x in shift_and_fronts(slot, mode)] + ["}"]
-                        + statements())
+                return (["if (k != k_next) {  // (re)load the full K-window"] + ["    " + x for x in dup(reload())]
+                        + ["} else {"] + ["    " + x for x in dup(shift_and_fronts(slot, mode))] + ["}"]
+                        + merged(statements()))
 
             def refill(slot, R, keys) -> List[str]:
                 body = []
@@ -970,23 +1020,24 @@ class ColumnGen:
                         o.append("        for (int k = ss + 1; k < se; ++k) {")
                     else:
                         o.append("        for (int k = se - 2; k >= ss; --k) {")
-                    o += ["            " + x for x in shift_and_fronts(None, mode) + statements()]
+                    o += ["            " + x for x in dup(shift_and_fronts(None, mode)) + merged(statements())]
                     o.append("        }")
                     o.append("    }")
                     o.append("}")
                     return o
+                pro = []
                 for u in range(R):
                     for key in keys:
                         fv = wvar(*key, front[key])
                         t = decl_dtype[key[0]].ctype
-                        o.append(f"        {t} rg{u}_{fv};")
-                        o += ["        " + x for x in load_into(f"rg{u}_{fv}", *key, f"{first} {step} {u} + ({front[key]})",
-                                                                maybe_cached=False)]
+                        pro.append(f"{t} rg{u}_{fv};")
+                        pro += load_into(f"rg{u}_{fv}", *key, f"{first} {step} {u} + ({front[key]})", maybe_cached=False)
+                o += ["        " + x for x in dup(pro)]
                 # first level: reload or continue; ring slot 0
                 o.append("        {")
                 o.append(f"            const int k = {first};")
                 o += ["            " + x for x in entry_level(0, mode)]
-                o += ["            " + x for x in refill(0, R, keys)]
+                o += ["            " + x for x in dup(refill(0, R, keys))]
                 o.append("        }")
                 # full blocks of R levels: shift only, no branches around loads (a load inside a
                 # branch makes the compiler drain every load in flight at the join)
@@ -1005,8 +1056,8 @@ class ColumnGen:
                         u, slot = g, (g + 1) % R
                         o.append(f"            {{  // ring slot {slot}")
                         o.append(f"                const int k = kb {step} {u};")
-                        o += ["                " + x for x in shift_and_fronts(slot, mode) + statements()
-                              + refill(slot, R, keys)]
+                        o += ["                " + x for x in dup(shift_and_fronts(slot, mode)) + merged(statements())
+                              + dup(refill(slot, R, keys))]
                         o.append("            }")
                         continue
                     # tile mode, several levels per LDS barrier: every level's statements before
@@ -1023,11 +1074,12 @@ class ColumnGen:
                         cut = next(q for q, x in enumerate(st) if x.startswith("gtmi::lds_barrier();"))
                         pre, post = st[:cut], st[cut + 1:]
                         names = sorted(set(_WVAR.findall("\n".join(post))))
-                        o += ["                " + ren(x) for x in shift_and_fronts(slot, mode) + pre]
-                        o += [f"                auto sn{b}_{n} = {n};" for n in names]
-                        o += ["                " + ren(x) for x in refill(slot, R, keys)]
+                        # pre[0] is the level's k_next update: once for both rows of a thread
+                        o += ["                " + ren(x) for x in dup(shift_and_fronts(slot, mode)) + pre[:1] + dup(pre[1:])]
+                        o += ["                " + x for x in dup([f"auto sn{b}_{n} = {n};" for n in names])]
+                        o += ["                " + ren(x) for x in dup(refill(slot, R, keys))]
                         snap = re.compile(r"\b(" + "|".join(map(re.escape, names)) + r")\b") if names else None
-                        posts += [ren(snap.sub(lambda m, b=b: f"sn{b}_{m.group(1)}", x) if snap else x) for x in post]
+                        posts += dup([ren(snap.sub(lambda m, b=b: f"sn{b}_{m.group(1)}", x) if snap else x) for x in post])
                     o.append("                gtmi::lds_barrier();  // the block's planes are complete")
                     o += ["                " + x for x in posts]
                     o.append("            }")
@@ -1038,7 +1090,7 @@ class ColumnGen:
                     cond = f"kb + {u} < se" if fwd else f"kb - {u} >= ss"
                     o.append(f"        if ({cond}) {{  // ring slot {slot}")
                     o.append(f"            const int k = kb {step} {u};")
-                    o += ["            " + x for x in shift_and_fronts(slot, mode) + statements()]
+                    o += ["            " + x for x in dup(shift_and_fronts(slot, mode)) + merged(statements())]
                     o.append("        }")
                 o.append("    }")
                 o.append("}")

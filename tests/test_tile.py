@@ -38,7 +38,9 @@ from stencil_cases import staged_forward_ij_temp as fwd_recurrence_ij_temp  # no
 # defaults, the aligned tile width and 64 or 128 lanes by cell size), levels per LDS barrier
 # (default 2 when a loop can be blocked)
 GEOMS = [(8, 0, 0), (4, 0, 0), (16, 0, 0), (8, 60, 64), (16, 13, 0), (4, 0, 128), (8, 100, 128),
-         (8, 0, 0, 1), (4, 0, 0, 4), (16, 0, 0, 1), (8, 60, 64, 4)]
+         (8, 0, 0, 1), (4, 0, 0, 4), (16, 0, 0, 1), (8, 60, 64, 4),
+         # (tile_by, tile_ti, tile_bx, tile_lblock, tile_rows): two rows per thread
+         (8, 0, 128, 2, 2), (4, 0, 0, 1, 2), (8, 60, 64, 4, 2)]
 
 # name: (definition, {field: (halo_i_lo, halo_i_hi, halo_j_lo, halo_j_hi)}, dtype)
 CASES = {name: (defn, halos, np.dtype(dt).type) for name, (defn, halos, dt) in TILE_PROGRAMS.items()}
@@ -227,6 +229,8 @@ def geom_opts(geom):
     opts = {"tile_by": tile_by, "tile_ti": tile_ti, "tile_bx": tile_bx}
     if len(geom) > 3:
         opts["tile_lblock"] = geom[3]
+    if len(geom) > 4:
+        opts["tile_rows"] = geom[4]
     return opts
 
 
