@@ -7,6 +7,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r06g}
 mkdir -p $O
-GTMI_NO_COMPILE=1 GTMI_FUZZ_NK=${FUZZ_NK:-0} GTMI_FUZZ_EXTRA=150 GTMI_FUZZ_V3=174 timeout -k 10 900 python -u -m pytest tests/test_fuzz.py -q -m gpu \
+GTMI_NO_COMPILE=1 GTMI_FUZZ_OPTS="$FUZZ_OPTS" GTMI_FUZZ_NK=${FUZZ_NK:-0} GTMI_FUZZ_EXTRA=150 GTMI_FUZZ_V3=174 timeout -k 10 900 python -u -m pytest tests/test_fuzz.py -q -m gpu \
   --timeout 120 --timeout-method thread -p no:cacheprovider > $O/fuzz_stress_nk${FUZZ_NK:-0}.log 2>&1
 rc=$?; tail -3 $O/fuzz_stress_nk${FUZZ_NK:-0}.log; exit $rc

@@ -3,6 +3,7 @@ must reproduce the numpy backend bit for bit. The CPU part checks that every pro
 runs on numpy and builds for gfx950; the GPU part compares results."""
 
 import importlib.util
+import json
 import os
 import sys
 
@@ -32,7 +33,10 @@ def _shape(seed):
 
 
 def _opts(seed):
-    return [{}, {"jchunk": 3}, {"jchunk": 8, "prefetch": 1}][seed % 3]
+    # stress runs: GTMI_FUZZ_OPTS (JSON) adds backend options to every program, e.g.
+    # '{"tile_rows": 2, "tile_bx": 128, "tile_by": 8}' for the two-row tile geometry
+    extra = json.loads(os.environ.get("GTMI_FUZZ_OPTS") or "{}")
+    return {**[{}, {"jchunk": 3}, {"jchunk": 8, "prefetch": 1}][seed % 3], **extra}
 
 
 def _load(seed, tmpdir):
