@@ -149,6 +149,21 @@ def test_tile_lds_planes_fit_the_cu():
     assert c.plan.scratch  # the staged lowering's phases
 
 
+def test_tile_rows_two_rows_per_thread():
+    """``tile_rows=2``: the block's threads cover twice ``tile_by`` rows (LDS planes and the launch
+    grid sized for it), each thread carrying a second column's state under ``_r1`` names; other
+    values are refused; the LDS budget counts both rows."""
+    c = _gen(fwd_recurrence_ij_temp, tile_rows=2, tile_bx=128, tile_by=8)
+    assert all(p[1:] == (16, 128) for p in _lds_planes(c.source)), _lds_planes(c.source)
+    assert "const int ty_r1 = ty + 8, j_r1 = j + 8;" in c.source
+    assert "dim3(128, 8)" in c.source and "(nj + 14) / 15" in c.source
+    assert "one LDS barrier" in c.source  # still blocked
+    with pytest.raises(ValueError, match="tile_rows"):
+        _gen(fwd_recurrence_ij_temp, tile_rows=3)
+    planes = _lds_planes(_gen(tile_many_planes, tile_rows=2, tile_by=8).source)
+    assert sum(8 * a * b * d for a, b, d in planes) <= 160 * 1024, planes
+
+
 def test_tile_levels_blocked_only_without_memory_raw():
     """A loop whose API output, stored after the barrier one level ahead, is read back before the
     next level's barrier keeps one level per barrier; the other tile programs are blocked
