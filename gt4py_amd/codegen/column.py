@@ -191,8 +191,8 @@ class ColumnGen:
                 by = 16 if self.ext[2] + self.ext[3] <= 1 and self._tile_item() >= 8 and self._by_cap >= 16 else 8
             # two waves per row for cells of 4 bytes or less (a row of 448 B of outputs, r03l sweep)
             bx = int(self.opts.get("tile_bx", 0)) or (128 if self._tile_item() <= 4 and by <= 8 else 64)
-            if by not in (4, 8, 16) or bx not in (64, 128) or bx * by > 1024:
-                raise ValueError(f"tile_bx x tile_by must be 64 or 128 x 4, 8 or 16 (at most 1024 threads), got {bx} x {by}")
+            if not 2 <= by <= 16 or bx not in (64, 128) or bx * by > 1024:
+                raise ValueError(f"tile_bx x tile_by must be 64 or 128 x 2 ... 16 (at most 1024 threads), got {bx} x {by}")
             return bx, by
         bx = int(self.opts.get("col_bx", COLUMN_BLOCK[0]))
         if bx not in (64, 128, 256):

@@ -40,7 +40,9 @@ from stencil_cases import staged_forward_ij_temp as fwd_recurrence_ij_temp  # no
 GEOMS = [(8, 0, 0), (4, 0, 0), (16, 0, 0), (8, 60, 64), (16, 13, 0), (4, 0, 128), (8, 100, 128),
          (8, 0, 0, 1), (4, 0, 0, 4), (16, 0, 0, 1), (8, 60, 64, 4),
          # (tile_by, tile_ti, tile_bx, tile_lblock, tile_rows): two rows per thread
-         (8, 0, 128, 2, 2), (4, 0, 0, 1, 2), (8, 60, 64, 4, 2)]
+         (8, 0, 128, 2, 2), (4, 0, 0, 1, 2), (8, 60, 64, 4, 2),
+         # row counts that are not powers of two
+         (12, 0, 0, 2, 2), (11, 0, 0)]
 
 # name: (definition, {field: (halo_i_lo, halo_i_hi, halo_j_lo, halo_j_hi)}, dtype)
 CASES = {name: (defn, halos, np.dtype(dt).type) for name, (defn, halos, dt) in TILE_PROGRAMS.items()}
