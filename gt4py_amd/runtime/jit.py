@@ -35,6 +35,11 @@ BASE_FLAGS = [
     "-fno-fast-math",
     "-fno-gpu-flush-denormals-to-zero",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
+    # keep every DPP wave rotate a separate v_mov_b32_dpp: folded into its consumer
+    # (v_subrev_u32_dpp ... wave_rol:1) it gave wrong lanes on gfx950 (scripts/lab/dpp_combine_lab.hip,
+    # DESIGN.md §3 K1 "I offsets"); tests/test_dpp_fold.py checks the generated code for it
+    "-mllvm",
+    "-amdgpu-dpp-combine=false",
     "-Wno-unused-variable",
     "-Wno-unused-but-set-variable",
 ]

@@ -103,10 +103,118 @@ def _generate_v3(seed):
     return "\n".join(L) + "\n", name
 
 
+MIXED_BASE = 9000  # seeds >= MIXED_BASE: mixed-precision programs (_generate_mixed)
+# field dtypes of the mixed-precision programs: f32 and f64 inputs, an int32 input, an f32 and an
+# f64 output (the NumPy-ufunc upcasting of gtir_upcaster.py:80-143 and the cast on assignment)
+MIXED_FIELDS = {"a": "float32", "b": "float64", "c": "float32", "m": "int32", "out1": "float32", "out2": "float64"}
+
+
+def field_dtypes(seed):
+    """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= MIXED_BASE:
+        return dict(MIXED_FIELDS)
+    return {n: "float64" for n in ("a", "b", "c", "out1", "out2")}
+
+
+def make_inputs(seed, shape):
+    """Deterministic inputs of program ``seed`` on domain ``shape``: (fields, origins). Inputs
+    carry an IJ halo of 2; float inputs U(-4, 4), the int32 input U{-5..5}, outputs U(-1, 1) in
+    their own dtype (cells outside the domain keep these values)."""
+    import numpy as np
+
+    rng = np.random.default_rng(20000 + seed)
+    ni, nj, nk = shape
+    dts = field_dtypes(seed)
+    fields, origin = {}, {}
+    for n, dt in dts.items():
+        if n.startswith("out"):
+            fields[n] = rng.uniform(-1, 1, (ni, nj, nk)).astype(dt)
+            origin[n] = (0, 0, 0)
+        elif dt == "int32":
+            fields[n] = rng.integers(-5, 6, (ni + 4, nj + 4, nk)).astype(dt)
+            origin[n] = (2, 2, 0)
+        else:
+            fields[n] = rng.uniform(-4, 4, (ni + 4, nj + 4, nk)).astype(dt)
+            origin[n] = (2, 2, 0)
+    return fields, origin
+
+
+class _MixedGen(_Gen):
+    """Leaves over f32/f64/int32 fields, float and int literals: every binary operation mixes
+    dtypes at random, so the program exercises the upcasting rules, not one precision."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if allow_temps and self.temps and r.random() < 0.35:
+            t = r.choice(self.temps)
+            di, dj = (r.randint(-1, 1), r.randint(-1, 1)) if allow_temps == "offsets" else (0, 0)
+            return f"{t}[{di}, {dj}, 0]"
+        x = r.random()
+        if x < 0.08:
+            return repr(round(r.uniform(-3, 3), 3))
+        if x < 0.14:
+            return str(r.randint(-3, 3))
+        f = r.choice(("a", "b", "c", "a", "c", "m"))
+        di, dj = r.randint(-1, 1), r.randint(-1, 1)
+        dk = r.choice((0, 0, 0, 1, -1)) if kmode == "kwin" else 0
+        return f"{f}[{di}, {dj}, {dk}]"
+
+
+def _generate_mixed(seed):
+    """Seeds >= MIXED_BASE: PARALLEL computations split into K intervals (K offsets in the middle
+    one), FORWARD/BACKWARD recurrences on temporaries whose dtype comes from their first
+    assignment (later f64 values are cast back), and conditionals, over f32, f64 and int32
+    fields with f64 and int literals."""
+    g = _MixedGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    for ci in range(r.randint(1, 3)):
+        order = r.choice(("PARALLEL", "PARALLEL", "FORWARD", "BACKWARD"))
+        out = r.choice(("out1", "out2"))
+        if order == "PARALLEL":
+            L.append("    with computation(PARALLEL):")
+            L.append("        with interval(0, 1):")
+            L.append(f"            {out} = {g.expr(2, False, 'par')}")
+            L.append("        with interval(1, -1):")
+            nst = r.randint(0, 2)
+            for si in range(nst):
+                t = f"t{ci}_{si}"
+                L.append(f"            {t} = {g.expr(2, True, 'kwin')}")
+                g.temps.append(t)
+            if r.random() < 0.5:
+                L.append(f"            if {g.expr(1, True, 'kwin')} > s:")
+                L.append(f"                {out} = {g.expr(2, 'offsets', 'kwin')}")
+                L.append("            else:")
+                L.append(f"                {out} = {g.expr(2, 'offsets', 'kwin')} * s")
+            else:
+                L.append(f"            {out} = {g.expr(3, 'offsets', 'kwin')}")
+            L.append("        with interval(-1, None):")
+            L.append(f"            {out} = {g.expr(2, False, 'par')} + {out}")
+            g.temps = []
+        else:
+            first, rest = ("interval(0, 1)", "interval(1, None)") if order == "FORWARD" else (
+                "interval(-1, None)", "interval(0, -1)")
+            dk = -1 if order == "FORWARD" else 1
+            acc = f"acc{ci}"
+            L.append(f"    with computation({order}):")
+            L.append(f"        with {first}:")
+            L.append(f"            {acc} = {g.expr(2, False, 'seq')}")
+            L.append(f"            {out} = {acc}")
+            L.append(f"        with {rest}:")
+            L.append(f"            {acc} = {acc}[0, 0, {dk}] * {round(r.uniform(0.25, 0.75), 2)} + {g.expr(2, False, 'seq')}")
+            L.append(f"            {out} = {acc} - {out}[0, 0, {dk}] * 0.25")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
-    seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``."""
+    seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
+    ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= MIXED_BASE:
+        return _generate_mixed(seed)
     if seed >= 7000:
         return _generate_v3(seed)
     v2 = seed >= 1000

@@ -21,6 +21,9 @@ SEEDS = list(range(60)) + list(range(1000, 1060))
 # the sweep-pair / tile templates (seeds 7000...)
 SEEDS += list(range(5000, 5000 + int(os.environ.get("GTMI_FUZZ_EXTRA", "0"))))
 SEEDS += list(range(7000, 7000 + int(os.environ.get("GTMI_FUZZ_V3", "24"))))
+# mixed-precision programs (f32/f64/int32 fields; also pinned to the reference at small domains,
+# tests/test_fuzz_reference.py)
+SEEDS += list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + int(os.environ.get("GTMI_FUZZ_MIXED", "160"))))
 
 
 def _shape(seed):
@@ -52,6 +55,10 @@ def _load(seed, tmpdir):
 
 
 def _inputs(seed):
+    if seed >= fuzz_stencils.MIXED_BASE:
+        fields, origin = fuzz_stencils.make_inputs(seed, _shape(seed))
+        return ({k: v for k, v in fields.items() if not k.startswith("out")},
+                {k: v for k, v in fields.items() if k.startswith("out")}, origin)
     rng = np.random.default_rng(1000 + seed)
     ni, nj, nk = _shape(seed)
     ins = {n: rng.uniform(-4, 4, (ni + 4, nj + 4, nk)) for n in ("a", "b", "c")}
@@ -92,8 +99,8 @@ def test_fuzz_program_matches_numpy(seed, tmp_path):
     ref = _run_numpy(defn, seed)
     st = gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"fuzz.hip.{seed}", **_opts(seed))
     ins, outs, origin = _inputs(seed)
-    dev = {k: storage.from_array(v, backend="gt:mi355x", aligned_index=(2, 2, 0)) for k, v in ins.items()}
-    dev.update({k: storage.from_array(v, backend="gt:mi355x") for k, v in outs.items()})
+    dev = {k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x", aligned_index=(2, 2, 0)) for k, v in ins.items()}
+    dev.update({k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x") for k, v in outs.items()})
     st(**dev, s=0.75, origin=origin, domain=_shape(seed))
     for k in ("out1", "out2"):
         got = storage.to_numpy(dev[k])
