@@ -4,10 +4,13 @@
 import fuzz_stencils
 
 # the default fuzz seeds (f64 programs: PARALLEL/FORWARD/BACKWARD, horizontal regions, staged
-# sweeps, sweep pairs and tile templates) and the mixed-precision programs
-N_MIXED = 160
+# sweeps, sweep pairs and tile templates), the mixed-precision, K-offset and
+# lower-dimensional-field programs
+N_MIXED, N_KOFF, N_LOWDIM = 160, 80, 60
 PINNED = list(range(60)) + list(range(1000, 1060)) + list(range(7000, 7024)) + list(
-    range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + N_MIXED))
+    range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + N_MIXED)) + list(
+    range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + N_KOFF)) + list(
+    range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + N_LOWDIM))
 
 
 def pinned_shape(seed):

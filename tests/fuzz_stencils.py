@@ -109,33 +109,49 @@ MIXED_BASE = 9000  # seeds >= MIXED_BASE: mixed-precision programs (_generate_mi
 MIXED_FIELDS = {"a": "float32", "b": "float64", "c": "float32", "m": "int32", "out1": "float32", "out2": "float64"}
 
 
+LOWDIM_BASE = 9700  # seeds >= LOWDIM_BASE: lower-dimensional fields (_generate_lowdim)
+LOWDIM_FIELDS = {"a": ("float64", "IJK"), "w": ("float32", "IJ"), "z": ("float64", "K"),
+                 "out1": ("float64", "IJK"), "out2": ("float64", "IJ")}
+
+
 def field_dtypes(seed):
     """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= LOWDIM_BASE:
+        return {n: t for n, (t, _) in LOWDIM_FIELDS.items()}
     if seed >= MIXED_BASE:
         return dict(MIXED_FIELDS)
     return {n: "float64" for n in ("a", "b", "c", "out1", "out2")}
 
 
+def field_axes(seed):
+    """{field: axes} ("IJK", "IJ" or "K") of the program ``generate(seed)`` writes."""
+    if seed >= LOWDIM_BASE:
+        return {n: ax for n, (_, ax) in LOWDIM_FIELDS.items()}
+    return {n: "IJK" for n in field_dtypes(seed)}
+
+
 def make_inputs(seed, shape):
     """Deterministic inputs of program ``seed`` on domain ``shape``: (fields, origins). Inputs
     carry an IJ halo of 2; float inputs U(-4, 4), the int32 input U{-5..5}, outputs U(-1, 1) in
-    their own dtype (cells outside the domain keep these values)."""
+    their own dtype (cells outside the domain keep these values). Lower-dimensional fields have
+    only their own axes."""
     import numpy as np
 
     rng = np.random.default_rng(20000 + seed)
     ni, nj, nk = shape
-    dts = field_dtypes(seed)
+    dts, axes = field_dtypes(seed), field_axes(seed)
     fields, origin = {}, {}
     for n, dt in dts.items():
-        if n.startswith("out"):
-            fields[n] = rng.uniform(-1, 1, (ni, nj, nk)).astype(dt)
-            origin[n] = (0, 0, 0)
+        out = n.startswith("out")
+        ext = {"I": ni if out else ni + 4, "J": nj if out else nj + 4, "K": nk}
+        shp = tuple(ext[a] for a in axes[n])
+        origin[n] = tuple(0 if (out or a == "K") else 2 for a in axes[n])
+        if out:
+            fields[n] = rng.uniform(-1, 1, shp).astype(dt)
         elif dt == "int32":
-            fields[n] = rng.integers(-5, 6, (ni + 4, nj + 4, nk)).astype(dt)
-            origin[n] = (2, 2, 0)
+            fields[n] = rng.integers(-5, 6, shp).astype(dt)
         else:
-            fields[n] = rng.uniform(-4, 4, (ni + 4, nj + 4, nk)).astype(dt)
-            origin[n] = (2, 2, 0)
+            fields[n] = rng.uniform(-4, 4, shp).astype(dt)
     return fields, origin
 
 
@@ -208,11 +224,119 @@ def _generate_mixed(seed):
     return "\n".join(L) + "\n", name
 
 
+KOFF_BASE = 9500  # seeds >= KOFF_BASE: K-offset programs (_generate_koff), mixed precision too
+
+
+class _KoffGen(_MixedGen):
+    """Leaves of the K-offset programs: ``kmode`` "k" reads fields (and the PARALLEL temporaries
+    in ``self.ktemps``) at K offsets -1..1, optionally at IJ offsets too."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if kmode == "k" and self.ktemps and r.random() < 0.3:
+            t = r.choice(self.ktemps)
+            di, dj = (r.randint(-1, 1), r.randint(-1, 1)) if r.random() < 0.3 else (0, 0)
+            return f"{t}[{di}, {dj}, {r.randint(-1, 1)}]"
+        if kmode == "k":
+            return super().leaf(allow_temps, "kwin")
+        return super().leaf(allow_temps, kmode)
+
+
+def _generate_koff(seed):
+    """Seeds >= KOFF_BASE: PARALLEL temporaries over the whole column, then a FORWARD or BACKWARD
+    sweep in three intervals whose middle one reads the fields and those temporaries at K
+    offsets (K windows of the column kernel, staged phases when read at IJ offsets), then
+    optionally a PARALLEL computation reading the temporaries at K offsets again."""
+    g = _KoffGen(seed)
+    g.ktemps = []
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    L.append("    with computation(PARALLEL), interval(...):")
+    for q in range(r.randint(1, 2)):
+        L.append(f"        p{q} = {g.expr(2, False, 'par')}")
+        g.ktemps.append(f"p{q}")
+    order = r.choice(("FORWARD", "BACKWARD"))
+    out = r.choice(("out1", "out2"))
+    first, last = ("interval(0, 1)", "interval(-1, None)") if order == "FORWARD" else ("interval(-1, None)", "interval(0, 1)")
+    dk = -1 if order == "FORWARD" else 1
+    L.append(f"    with computation({order}):")
+    L.append(f"        with {first}:")
+    L.append(f"            acc = {g.expr(2, False, 'par')} + p0")
+    L.append(f"            {out} = acc")
+    L.append("        with interval(1, -1):")
+    L.append(f"            acc = acc[0, 0, {dk}] * {round(r.uniform(0.25, 0.75), 2)} + {g.expr(2, False, 'k')}")
+    if r.random() < 0.5:
+        L.append(f"            if {g.expr(1, False, 'k')} > s:")
+        L.append(f"                {out} = acc - {out}[0, 0, {dk}] * 0.25")
+        L.append("            else:")
+        L.append(f"                {out} = {g.expr(1, False, 'k')} + acc")
+    else:
+        L.append(f"            {out} = acc - {out}[0, 0, {dk}] * 0.25")
+    L.append(f"        with {last}:")
+    L.append(f"            acc = acc[0, 0, {dk}] * 0.5 + {g.expr(1, False, 'par')}")
+    L.append(f"            {out} = acc * s")
+    if r.random() < 0.6:
+        other = "out2" if out == "out1" else "out1"
+        L.append("    with computation(PARALLEL), interval(1, -1):")
+        L.append(f"        {other} = {g.expr(3, False, 'k')}")
+    return "\n".join(L) + "\n", name
+
+
+class _LowdimGen(_Gen):
+    """Leaves over a 3-D f64 field ``a``, a 2-D f32 field ``w`` and a 1-D K field ``z``."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        x = r.random()
+        if x < 0.1:
+            return repr(round(r.uniform(-3, 3), 3))
+        if x < 0.45:
+            dk = r.choice((0, 0, 1, -1)) if kmode == "kwin" else 0
+            return f"a[{r.randint(-1, 1)}, {r.randint(-1, 1)}, {dk}]"
+        if x < 0.75:
+            return f"w[{r.randint(-1, 1)}, {r.randint(-1, 1)}]"
+        return f"z[{r.choice((0, 0, 1, -1)) if kmode == 'kwin' else 0}]"
+
+
+def _generate_lowdim(seed):
+    """Seeds >= LOWDIM_BASE: 2-D (IJ) and 1-D (K) fields read beside a 3-D one (K offsets of the
+    K field in the middle interval), a 2-D output accumulated by a FORWARD sweep and optionally
+    read back by a later PARALLEL computation."""
+    g = _LowdimGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    ann = {"IJK": "Field[np.{t}]", "IJ": "Field[IJ, np.{t}]", "K": "Field[K, np.{t}]"}
+    sig = ", ".join(f"{n}: " + ann[ax].format(t=t) for n, (t, ax) in LOWDIM_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    L.append("    with computation(PARALLEL):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            out1 = {g.expr(2, False, 'par')}")
+    L.append("        with interval(1, -1):")
+    L.append(f"            out1 = {g.expr(3, False, 'kwin')}")
+    L.append("        with interval(-1, None):")
+    L.append(f"            out1 = {g.expr(2, False, 'par')} * s")
+    L.append("    with computation(FORWARD):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            out2 = {g.expr(2, False, 'par')}")
+    L.append("        with interval(1, None):")
+    L.append(f"            out2 = out2 * {round(r.uniform(0.25, 0.75), 2)} + {g.expr(2, False, 'par')}")
+    if r.random() < 0.5:
+        L.append("    with computation(PARALLEL), interval(...):")
+        L.append(f"        out1 = out1 + out2 * {g.expr(1, False, 'par')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= LOWDIM_BASE:
+        return _generate_lowdim(seed)
+    if seed >= KOFF_BASE:
+        return _generate_koff(seed)
     if seed >= MIXED_BASE:
         return _generate_mixed(seed)
     if seed >= 7000:

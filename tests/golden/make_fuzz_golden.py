@@ -30,7 +30,7 @@ import types
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 HEADER = """import numpy as np
-from gt4py_amd.gtscript import BACKWARD, FORWARD, PARALLEL, Field, I, J, computation, horizontal, interval, region
+from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
 
 """
 

@@ -13,7 +13,7 @@ import pytest
 import fuzz_stencils
 
 HEADER = """import numpy as np
-from gt4py_amd.gtscript import BACKWARD, FORWARD, PARALLEL, Field, I, J, computation, horizontal, interval, region
+from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
 
 """
 SEEDS = list(range(60)) + list(range(1000, 1060))
@@ -24,6 +24,10 @@ SEEDS += list(range(7000, 7000 + int(os.environ.get("GTMI_FUZZ_V3", "24"))))
 # mixed-precision programs (f32/f64/int32 fields; also pinned to the reference at small domains,
 # tests/test_fuzz_reference.py)
 SEEDS += list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + int(os.environ.get("GTMI_FUZZ_MIXED", "160"))))
+# K-offset programs (PARALLEL temporaries read at K offsets by a three-interval sweep)
+SEEDS += list(range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + int(os.environ.get("GTMI_FUZZ_KOFF", "80"))))
+# lower-dimensional fields (IJ and K inputs, an IJ output of a FORWARD sweep)
+SEEDS += list(range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + int(os.environ.get("GTMI_FUZZ_LOWDIM", "60"))))
 
 
 def _shape(seed):
@@ -67,6 +71,15 @@ def _inputs(seed):
     return ins, outs, origin
 
 
+def to_device(fields, origin, seed):
+    """gt:mi355x storages of the program's fields, aligned at their origins, with their axes."""
+    from gt4py_amd import storage
+
+    axes = fuzz_stencils.field_axes(seed)
+    return {k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x", aligned_index=origin[k],
+                                  dimensions=tuple(axes[k])) for k, v in fields.items()}
+
+
 def _run_numpy(defn, seed):
     from gt4py_amd import gtscript
 
@@ -99,8 +112,7 @@ def test_fuzz_program_matches_numpy(seed, tmp_path):
     ref = _run_numpy(defn, seed)
     st = gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"fuzz.hip.{seed}", **_opts(seed))
     ins, outs, origin = _inputs(seed)
-    dev = {k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x", aligned_index=(2, 2, 0)) for k, v in ins.items()}
-    dev.update({k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x") for k, v in outs.items()})
+    dev = to_device({**ins, **outs}, origin, seed)
     st(**dev, s=0.75, origin=origin, domain=_shape(seed))
     for k in ("out1", "out2"):
         got = storage.to_numpy(dev[k])

@@ -20,7 +20,7 @@ from fuzz_pinned import PINNED, pinned_shape
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = """import numpy as np
-from gt4py_amd.gtscript import BACKWARD, FORWARD, PARALLEL, Field, I, J, computation, horizontal, interval, region
+from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
 
 """
 
@@ -88,6 +88,6 @@ def test_mi355x_matches_reference(seed, tmp_path):
     st = gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"fuzz.hip.{seed}", **test_fuzz._opts(seed))
     assert torch.cuda.is_available(), "gt:mi355x needs a ROCm device"
     fields, origin = fuzz_stencils.make_inputs(seed, pinned_shape(seed))
-    dev = {k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x", aligned_index=origin[k]) for k, v in fields.items()}
+    dev = test_fuzz.to_device(fields, origin, seed)
     st(**dev, s=0.75, origin=origin, domain=pinned_shape(seed))
     _check(seed, src, rec, {k: storage.to_numpy(v) for k, v in dev.items()})
