@@ -116,6 +116,8 @@ LOWDIM_FIELDS = {"a": ("float64", "IJK"), "w": ("float32", "IJ"), "z": ("float64
 
 def field_dtypes(seed):
     """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= OPS_BASE:
+        return dict(MIXED_FIELDS)
     if seed >= LOWDIM_BASE:
         return {n: t for n, (t, _) in LOWDIM_FIELDS.items()}
     if seed >= MIXED_BASE:
@@ -125,7 +127,7 @@ def field_dtypes(seed):
 
 def field_axes(seed):
     """{field: axes} ("IJK", "IJ" or "K") of the program ``generate(seed)`` writes."""
-    if seed >= LOWDIM_BASE:
+    if LOWDIM_BASE <= seed < OPS_BASE:
         return {n: ax for n, (_, ax) in LOWDIM_FIELDS.items()}
     return {n: "IJK" for n in field_dtypes(seed)}
 
@@ -328,11 +330,94 @@ def _generate_lowdim(seed):
     return "\n".join(L) + "\n", name
 
 
+OPS_BASE = 9800  # seeds >= OPS_BASE: operator programs (_generate_ops), mixed precision
+
+
+class _OpsGen(_MixedGen):
+    """Expressions over the exactly rounded builtins: mod, ** 2, sqrt, floor/ceil/trunc, round
+    (half to even), round_away_from_zero, casts; conditions with and/or/not."""
+
+    def expr(self, depth, allow_temps, kmode):
+        r = self.r
+        if depth == 0 or r.random() < 0.2:
+            return self.leaf(allow_temps, kmode)
+        x = self.expr(depth - 1, allow_temps, kmode)
+        k = r.random()
+        if k < 0.3:
+            return f"({x} {r.choice(('+', '-', '*'))} {self.expr(depth - 1, allow_temps, kmode)})"
+        if k < 0.38:
+            return f"({x} % (abs({self.expr(depth - 1, allow_temps, kmode)}) + 0.75))"
+        if k < 0.43:
+            return f"((m[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0] + {r.randint(0, 9)}) % {r.randint(2, 5)})"
+        if k < 0.5:
+            return f"(min(max({x}, -30.0), 30.0) ** 2)"
+        if k < 0.55:
+            return f"sqrt(abs({x}))"
+        if k < 0.67:
+            fn = r.choice(("floor", "ceil", "trunc", "round", "round_away_from_zero"))
+            return f"{fn}({x} * {r.choice((0.5, 1.5, 2.0, 0.25))})"
+        if k < 0.72:
+            ct = r.choice(("float32", "float64", "int32", "int64"))
+            return f"{ct}(min(max({x}, -100.0), 100.0))"
+        if k < 0.82:
+            return f"{r.choice(('min', 'max'))}({x}, {self.expr(depth - 1, allow_temps, kmode)})"
+        if k < 0.92:
+            return f"({x} if {self.cond(allow_temps, kmode)} else {self.expr(depth - 1, allow_temps, kmode)})"
+        return f"abs({x})"
+
+    def cond(self, allow_temps, kmode):
+        r = self.r
+        a = f"{self.expr(1, allow_temps, kmode)} {r.choice(('>', '<', '>=', '<=', '==', '!='))} {self.expr(1, allow_temps, kmode)}"
+        k = r.random()
+        if k < 0.5:
+            return a
+        b = f"{self.expr(1, allow_temps, kmode)} > {self.expr(0, allow_temps, kmode)}"
+        if k < 0.7:
+            return f"({a}) and (not ({b}))"
+        if k < 0.9:
+            return f"({a}) or ({b})"
+        return f"isfinite({self.expr(1, allow_temps, kmode)}) and ({a})"
+
+
+def _generate_ops(seed):
+    """Seeds >= OPS_BASE: PARALLEL if/elif/else chains (nested once) and a FORWARD sweep over the
+    operator set of ``_OpsGen``, on the mixed-precision fields."""
+    g = _OpsGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    out = r.choice(("out1", "out2"))
+    L.append("    with computation(PARALLEL), interval(...):")
+    L.append(f"        t0 = {g.expr(2, False, 'par')}")
+    g.temps.append("t0")
+    L.append(f"        if {g.cond(True, 'par')}:")
+    L.append(f"            {out} = {g.expr(2, True, 'par')}")
+    if r.random() < 0.5:
+        L.append(f"            if {g.cond(True, 'par')}:")
+        L.append(f"                {out} = {out} * {g.expr(1, True, 'par')}")
+    L.append(f"        elif {g.cond(True, 'par')}:")
+    L.append(f"            {out} = {g.expr(2, True, 'par')}")
+    L.append("        else:")
+    L.append(f"            {out} = {g.expr(2, True, 'par')} + s")
+    g.temps = []
+    if r.random() < 0.6:
+        other = "out2" if out == "out1" else "out1"
+        L.append("    with computation(FORWARD):")
+        L.append("        with interval(0, 1):")
+        L.append(f"            {other} = {g.expr(2, False, 'seq')}")
+        L.append("        with interval(1, None):")
+        L.append(f"            {other} = {other}[0, 0, -1] * 0.5 + {g.expr(2, False, 'seq')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= OPS_BASE:
+        return _generate_ops(seed)
     if seed >= LOWDIM_BASE:
         return _generate_lowdim(seed)
     if seed >= KOFF_BASE:

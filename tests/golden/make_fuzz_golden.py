@@ -31,6 +31,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 HEADER = """import numpy as np
 from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
+from gt4py_amd.gtscript import (ceil, float32, float64, floor, int32, int64, isfinite, isnan, round,
+                               round_away_from_zero, sqrt, trunc)
 
 """
 

@@ -14,6 +14,8 @@ import fuzz_stencils
 
 HEADER = """import numpy as np
 from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
+from gt4py_amd.gtscript import (ceil, float32, float64, floor, int32, int64, isfinite, isnan, round,
+                               round_away_from_zero, sqrt, trunc)
 
 """
 SEEDS = list(range(60)) + list(range(1000, 1060))
@@ -28,6 +30,8 @@ SEEDS += list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + int(os.
 SEEDS += list(range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + int(os.environ.get("GTMI_FUZZ_KOFF", "80"))))
 # lower-dimensional fields (IJ and K inputs, an IJ output of a FORWARD sweep)
 SEEDS += list(range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + int(os.environ.get("GTMI_FUZZ_LOWDIM", "60"))))
+# operator programs (mod, ** 2, sqrt, floor/ceil/trunc/round, casts, if/elif/else with and/or/not)
+SEEDS += list(range(fuzz_stencils.OPS_BASE, fuzz_stencils.OPS_BASE + int(os.environ.get("GTMI_FUZZ_OPS", "100"))))
 
 
 def _shape(seed):
