@@ -20,6 +20,27 @@ PINNED = list(range(60)) + list(range(1000, 1060)) + list(range(7000, 7024)) + l
 PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED]
 
 
+# the same programs at >= 98 levels, where the column kernels switch on their register band, LDS
+# tail cache and head/tail placement and tile kernels block levels: the sweep templates (sweep
+# pairs and tiles, K-offset sweeps) and the first 40 mixed-precision programs
+DEEP = [s for s in list(range(7000, 7024)) + list(range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + N_KOFF))
+        + list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + 40)) if s not in REFERENCE_REFUSED]
+# golden record keys: "<seed>" at pinned_shape(seed), "<seed>@deep" at deep_shape(seed)
+CASES = [(s, False) for s in PINNED] + [(s, True) for s in DEEP]
+
+
 def pinned_shape(seed):
     """Small domains: odd seeds a width that is not a multiple of any lane or tile width."""
     return (13, 11, 8) if seed % 2 == 0 else (21, 9, 7)
+
+
+def deep_shape(seed):
+    return (13, 11, 120) if seed % 2 == 0 else (21, 9, 121)
+
+
+def case_key(seed, deep):
+    return f"{seed}@deep" if deep else str(seed)
+
+
+def case_shape(seed, deep):
+    return deep_shape(seed) if deep else pinned_shape(seed)

@@ -6,7 +6,8 @@ tests/golden/make_golden.py)::
     PYTHONPATH=/tmp/gtoracle:/root/reference/src:/root/repo GT_CACHE_ROOT=/tmp/gtcache \
         python3 -W ignore tests/golden/make_fuzz_golden.py
 
-For every seed of ``tests/fuzz_pinned.py::PINNED`` this script generates the program with
+For every case of ``tests/fuzz_pinned.py::CASES`` (each pinned seed at a small domain, the
+sweep programs of ``DEEP`` again at >= 120 levels) this script generates the program with
 ``tests/fuzz_stencils.generate``, parses and builds it with the reference frontend and its numpy
 backend (``src/gt4py/cartesian/backend/numpy_backend.py``), runs it on
 ``fuzz_stencils.make_inputs(seed, shape)`` and records, per output field, the SHA-256 of the
@@ -63,25 +64,26 @@ def main():
     ref_gtscript = _alias_reference()
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import fuzz_stencils as fs
-    from fuzz_pinned import PINNED, pinned_shape
+    from fuzz_pinned import CASES, case_key, case_shape
 
     out = {}
     with tempfile.TemporaryDirectory() as tmp:
-        for seed in PINNED:
+        for seed, deep in CASES:
             src, name = fs.generate(seed)
-            rec = {"source_sha256": hashlib.sha256(src.encode()).hexdigest(), "shape": list(pinned_shape(seed))}
+            shape = case_shape(seed, deep)
+            rec = {"source_sha256": hashlib.sha256(src.encode()).hexdigest(), "shape": list(shape)}
             try:
                 defn = _load(src, name, tmp, seed)
                 st = ref_gtscript.stencil(backend="numpy", definition=defn, name=f"fuzzref.s{seed}", rebuild=False)
-                fields, origin = fs.make_inputs(seed, pinned_shape(seed))
-                st(**fields, s=0.75, origin=origin, domain=pinned_shape(seed))
+                fields, origin = fs.make_inputs(seed, shape)
+                st(**fields, s=0.75, origin=origin, domain=shape)
             except Exception as ex:  # the reference refuses the program: record it
                 rec["refused"] = type(ex).__name__
                 print(f"[refused] {seed}: {type(ex).__name__}: {str(ex).splitlines()[0][:120]}")
             else:
                 rec["outputs"] = {k: {"dtype": str(fields[k].dtype), "sha256": hashlib.sha256(fields[k].tobytes()).hexdigest()}
                                   for k in ("out1", "out2")}
-            out[str(seed)] = rec
+            out[case_key(seed, deep)] = rec
     with open(os.path.join(HERE, "fuzz_reference.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(f"{len(out)} programs, {sum('refused' in r for r in out.values())} refused")

@@ -1,4 +1,4 @@
-"""Differential-fuzz programs pinned to the REFERENCE: for every seed of ``fuzz_pinned.PINNED``,
+"""Differential-fuzz programs pinned to the REFERENCE: for every case of ``fuzz_pinned.CASES``,
 the output arrays of the reference numpy backend (``tests/golden/fuzz_reference.json``, SHA-256 of
 the bytes, made by ``tests/golden/make_fuzz_golden.py``) must be reproduced bit for bit -- by our
 numpy backend on the CPU and by gt:mi355x on the GPU. The f64 programs are the default fuzz seeds
@@ -16,7 +16,7 @@ import sys
 import pytest
 
 import fuzz_stencils
-from fuzz_pinned import PINNED, pinned_shape
+from fuzz_pinned import CASES, case_key, case_shape
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = """import numpy as np
@@ -42,8 +42,8 @@ def _load(seed, tmpdir):
     return getattr(mod, name), src
 
 
-def _golden(seed, src):
-    rec = GOLDEN.get(str(seed))
+def _golden(seed, deep, src):
+    rec = GOLDEN.get(case_key(seed, deep))
     assert rec is not None, f"seed {seed} has no reference record: run tests/golden/make_fuzz_golden.py"
     assert rec["source_sha256"] == hashlib.sha256(src.encode()).hexdigest(), (
         f"seed {seed}: the generator now writes a different program than the one pinned")
@@ -59,37 +59,43 @@ def _check(seed, src, rec, arrays):
             f"seed {seed} field {k} differs from the reference numpy backend:\n{src}")
 
 
+def _id(case):
+    return case_key(*case)
+
+
 def test_every_pinned_seed_has_a_reference_record():
-    assert sorted(GOLDEN) == sorted(str(s) for s in PINNED)
+    assert sorted(GOLDEN) == sorted(case_key(*c) for c in CASES)
     assert not [s for s, r in GOLDEN.items() if "refused" in r]
 
 
-@pytest.mark.parametrize("seed", PINNED)
-def test_numpy_backend_matches_reference(seed, tmp_path):
+@pytest.mark.parametrize("case", CASES, ids=_id)
+def test_numpy_backend_matches_reference(case, tmp_path):
     from gt4py_amd import gtscript
 
+    seed, deep = case
     defn, src = _load(seed, str(tmp_path))
-    rec = _golden(seed, src)
+    rec = _golden(seed, deep, src)
     st = gtscript.stencil(backend="numpy", definition=defn, name=f"fuzzpin.np.{seed}")
-    fields, origin = fuzz_stencils.make_inputs(seed, pinned_shape(seed))
-    st(**fields, s=0.75, origin=origin, domain=pinned_shape(seed))
+    fields, origin = fuzz_stencils.make_inputs(seed, case_shape(seed, deep))
+    st(**fields, s=0.75, origin=origin, domain=case_shape(seed, deep))
     _check(seed, src, rec, fields)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", PINNED)
-def test_mi355x_matches_reference(seed, tmp_path):
+@pytest.mark.parametrize("case", CASES, ids=_id)
+def test_mi355x_matches_reference(case, tmp_path):
     import torch
 
     from gt4py_amd import gtscript, storage
     import test_fuzz
 
+    seed, deep = case
     defn, src = _load(seed, str(tmp_path))
-    rec = _golden(seed, src)
+    rec = _golden(seed, deep, src)
     # the library of tests/test_fuzz.py (same program, same options): prebuilt by build()
     st = gtscript.stencil(backend="gt:mi355x", definition=defn, name=f"fuzz.hip.{seed}", **test_fuzz._opts(seed))
     assert torch.cuda.is_available(), "gt:mi355x needs a ROCm device"
-    fields, origin = fuzz_stencils.make_inputs(seed, pinned_shape(seed))
+    fields, origin = fuzz_stencils.make_inputs(seed, case_shape(seed, deep))
     dev = test_fuzz.to_device(fields, origin, seed)
-    st(**dev, s=0.75, origin=origin, domain=pinned_shape(seed))
+    st(**dev, s=0.75, origin=origin, domain=case_shape(seed, deep))
     _check(seed, src, rec, {k: storage.to_numpy(v) for k, v in dev.items()})
