@@ -411,11 +411,56 @@ def _generate_ops(seed):
     return "\n".join(L) + "\n", name
 
 
+CTRL_BASE = 9900  # seeds >= CTRL_BASE: while loops and horizontal regions (_generate_ctrl)
+REGIONS = ("region[I[0] : I[0] + 2, :]", "region[:, J[-1] - 1 : J[-1]]", "region[I[0] : I[0] + 3, J[0] : J[0] + 2]",
+           "region[I[-1] - 2 : I[-1], :]", "region[I[0] + 1 : I[-1] - 1, J[0] + 1 : J[0] + 2]")
+
+
+def _generate_ctrl(seed):
+    """Seeds >= CTRL_BASE: bounded while loops on temporaries (an int counter, optionally a value
+    condition), horizontal regions in PARALLEL and FORWARD/BACKWARD computations, over the
+    mixed-precision fields."""
+    g = _MixedGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    out = r.choice(("out1", "out2"))
+    other = "out2" if out == "out1" else "out1"
+    L.append("    with computation(PARALLEL), interval(...):")
+    L.append("        n = 0")
+    L.append(f"        acc = {g.expr(2, False, 'par')}")
+    cond = f"n < {r.randint(1, 4)}"
+    if r.random() < 0.5:
+        cond += f" and acc {r.choice(('>', '<'))} {round(r.uniform(-2, 2), 2)}"
+    L.append(f"        while {cond}:")
+    L.append(f"            acc = acc * {round(r.uniform(0.25, 0.75), 2)} + {g.expr(2, False, 'par')}")
+    L.append("            n = n + 1")
+    L.append(f"        {out} = acc + n")
+    if r.random() < 0.7:
+        L.append(f"        with horizontal({r.choice(REGIONS)}):")
+        L.append(f"            {out} = {g.expr(2, False, 'par')} + {out}")
+    order = r.choice(("FORWARD", "BACKWARD"))
+    first, rest = ("interval(0, 1)", "interval(1, None)") if order == "FORWARD" else ("interval(-1, None)", "interval(0, -1)")
+    dk = -1 if order == "FORWARD" else 1
+    L.append(f"    with computation({order}):")
+    L.append(f"        with {first}:")
+    L.append(f"            {other} = {g.expr(2, False, 'seq')}")
+    L.append(f"        with {rest}:")
+    L.append(f"            {other} = {other}[0, 0, {dk}] * 0.5 + {g.expr(2, False, 'seq')}")
+    if r.random() < 0.7:
+        L.append(f"            with horizontal({r.choice(REGIONS)}):")
+        L.append(f"                {other} = {g.expr(2, False, 'seq')} - {other}[0, 0, {dk}]")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= CTRL_BASE:
+        return _generate_ctrl(seed)
     if seed >= OPS_BASE:
         return _generate_ops(seed)
     if seed >= LOWDIM_BASE:

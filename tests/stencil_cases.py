@@ -2071,6 +2071,26 @@ case("abs_k_conditional", fields={"in_field": fs(5, 4, 6, init=("ramp", -5.0, 5.
      features=("golden_debug",))(abs_k_conditional)
 
 
+def while_value_condition(a: F64, b: F64, out: F64):
+    # a while loop whose condition reads a value its body changes before the counter: per point
+    # the counter is incremented with the OLD condition (debug and GridTools backends); the
+    # reference numpy backend re-evaluates the condition as the mask of `n = n + 1`
+    # (oir_to_npir.py:176-185) and skips the increment once acc has left the range
+    with computation(PARALLEL), interval(...):
+        n = 0
+        acc = a[0, 0, 0]
+        while n < 3 and acc < 1.0:
+            acc = acc * 0.5 + b[1, 0, 0]
+            n = n + 1
+        out = acc + n * 10.0
+
+
+case("while_value_condition", fields={"a": fs(9, 5, 4), "b": fs(9, 5, 4, init=("u", -1.0, 2.0)),
+                                      "out": fs(8, 5, 4, init="zeros")},
+     origin={"a": (0, 0, 0), "b": (0, 0, 0), "out": (0, 0, 0)}, domain=(8, 5, 4),
+     features=("golden_debug",))(while_value_condition)
+
+
 # --------------------------------------------------------------------------------------
 # Remaining stencil_definitions.py programs: every data type, a region with a conditional
 # --------------------------------------------------------------------------------------

@@ -32,6 +32,8 @@ SEEDS += list(range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + int(os.en
 SEEDS += list(range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + int(os.environ.get("GTMI_FUZZ_LOWDIM", "60"))))
 # operator programs (mod, ** 2, sqrt, floor/ceil/trunc/round, casts, if/elif/else with and/or/not)
 SEEDS += list(range(fuzz_stencils.OPS_BASE, fuzz_stencils.OPS_BASE + int(os.environ.get("GTMI_FUZZ_OPS", "100"))))
+# bounded while loops and horizontal regions in PARALLEL and sequential computations
+SEEDS += list(range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + int(os.environ.get("GTMI_FUZZ_CTRL", "100"))))
 
 
 def _shape(seed):
