@@ -5,9 +5,9 @@ import fuzz_stencils
 
 # the default fuzz seeds (f64 programs: PARALLEL/FORWARD/BACKWARD, horizontal regions, staged
 # sweeps, sweep pairs and tile templates), the mixed-precision, K-offset,
-# lower-dimensional-field, operator and
-# while-loop / horizontal-region programs
-N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL = 160, 80, 60, 100, 100
+# lower-dimensional-field, operator,
+# while-loop / horizontal-region and mixed tile programs
+N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE = 160, 80, 60, 100, 100, 60
 # programs the reference refuses: its upcaster raises "Type mismatch in `BinaryOp`. Types are
 # FLOAT32, INT64" on a comparison of sqrt(<int64>) (typed float32, as ours types it too) with an
 # int64; gt:mi355x accepts them. tests/test_fuzz.py still runs them against our
@@ -26,7 +26,8 @@ PINNED = list(range(60)) + list(range(1000, 1060)) + list(range(7000, 7024)) + l
     range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + N_KOFF)) + list(
     range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + N_LOWDIM)) + list(
     range(fuzz_stencils.OPS_BASE, fuzz_stencils.OPS_BASE + N_OPS)) + list(
-    range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + N_CTRL))
+    range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + N_CTRL)) + list(
+    range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + N_TILE))
 PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED | REFERENCE_DIVERGENT]
 
 
@@ -34,7 +35,8 @@ PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED | REFERENCE_DIVERGENT]
 # tail cache and head/tail placement and tile kernels block levels: the sweep templates (sweep
 # pairs and tiles, K-offset sweeps) and the first 40 mixed-precision programs
 DEEP = [s for s in list(range(7000, 7024)) + list(range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + N_KOFF))
-        + list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + 40)) if s in PINNED]
+        + list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + 40))
+        + list(range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + 30)) if s in PINNED]
 # golden record keys: "<seed>" at pinned_shape(seed), "<seed>@deep" at deep_shape(seed)
 CASES = [(s, False) for s in PINNED] + [(s, True) for s in DEEP]
 

@@ -114,8 +114,19 @@ LOWDIM_FIELDS = {"a": ("float64", "IJK"), "w": ("float32", "IJ"), "z": ("float64
                  "out1": ("float64", "IJK"), "out2": ("float64", "IJ")}
 
 
+TILE_BASE = 10000  # seeds >= TILE_BASE: mixed-precision tile programs with a vector field (_generate_tile)
+TILE_FIELDS = {**MIXED_FIELDS, "v": "float64"}  # v: 2 data components per cell
+
+
+def data_dims(seed):
+    """{field: trailing data-dimension shape} of the fields that have data dimensions."""
+    return {"v": (2,)} if seed >= TILE_BASE else {}
+
+
 def field_dtypes(seed):
     """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= TILE_BASE:
+        return dict(TILE_FIELDS)
     if seed >= OPS_BASE:
         return dict(MIXED_FIELDS)
     if seed >= LOWDIM_BASE:
@@ -143,10 +154,11 @@ def make_inputs(seed, shape):
     ni, nj, nk = shape
     dts, axes = field_dtypes(seed), field_axes(seed)
     fields, origin = {}, {}
+    dd = data_dims(seed)
     for n, dt in dts.items():
         out = n.startswith("out")
         ext = {"I": ni if out else ni + 4, "J": nj if out else nj + 4, "K": nk}
-        shp = tuple(ext[a] for a in axes[n])
+        shp = tuple(ext[a] for a in axes[n]) + dd.get(n, ())
         origin[n] = tuple(0 if (out or a == "K") else 2 for a in axes[n])
         if out:
             fields[n] = rng.uniform(-1, 1, shp).astype(dt)
@@ -454,11 +466,51 @@ def _generate_ctrl(seed):
     return "\n".join(L) + "\n", name
 
 
+class _TileGen(_MixedGen):
+    """Mixed-precision leaves plus the components of the vector field ``v``."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if r.random() < 0.2:
+            return f"v[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0][{r.randint(0, 1)}]"
+        return super().leaf(allow_temps, kmode)
+
+
+def _generate_tile(seed):
+    """Seeds >= TILE_BASE: the tile-kernel shape (a FORWARD recurrence whose product a second
+    FORWARD computation reads across columns, IJ caches in LDS) with an f32, f64 or int32
+    recurrence, mixed-precision operands and the components of a vector field."""
+    g = _TileGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items()) + ", v: Field[(np.float64, (2,))]"
+    L = [f"def {name}({sig}, *, s: float):"]
+    seedexpr = r.choice(("a[0, 0, 0]", "c[0, 0, 0] * 0.5", "m[0, 0, 0]", "b[0, 0, 0]", "v[0, 0, 0][1]"))
+    L.append("    with computation(FORWARD):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            ss = {seedexpr}")
+    L.append("        with interval(1, None):")
+    L.append(f"            ss = ss[0, 0, -1] * {round(r.uniform(0.25, 0.75), 2)} + {g.expr(2, False, 'seq')}")
+    L.append("    with computation(FORWARD), interval(...):")
+    L.append(f"        tt = ss * {round(r.uniform(0.5, 2), 3)} + {g.expr(1, False, 'seq')}")
+    offs = [(1, 0), (-1, 0), (0, 1), (0, -1), (1, 1), (-1, -1), (1, -1)]
+    picks = r.sample(offs, r.randint(2, 4))
+    terms = " + ".join(f"tt[{di}, {dj}, 0]" for di, dj in picks)
+    out = r.choice(("out1", "out2"))
+    L.append(f"        {out} = {terms} - ss * {g.expr(1, False, 'seq')}")
+    if r.random() < 0.5:
+        other = "out2" if out == "out1" else "out1"
+        L.append(f"        {other} = tt[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0] * v[0, 0, 0][0] + ss")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= TILE_BASE:
+        return _generate_tile(seed)
     if seed >= CTRL_BASE:
         return _generate_ctrl(seed)
     if seed >= OPS_BASE:

@@ -34,6 +34,8 @@ SEEDS += list(range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + int(o
 SEEDS += list(range(fuzz_stencils.OPS_BASE, fuzz_stencils.OPS_BASE + int(os.environ.get("GTMI_FUZZ_OPS", "100"))))
 # bounded while loops and horizontal regions in PARALLEL and sequential computations
 SEEDS += list(range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + int(os.environ.get("GTMI_FUZZ_CTRL", "100"))))
+# tile-kernel shape with mixed precision and a vector field
+SEEDS += list(range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + int(os.environ.get("GTMI_FUZZ_TILE", "60"))))
 
 
 def _shape(seed):
@@ -81,9 +83,9 @@ def to_device(fields, origin, seed):
     """gt:mi355x storages of the program's fields, aligned at their origins, with their axes."""
     from gt4py_amd import storage
 
-    axes = fuzz_stencils.field_axes(seed)
-    return {k: storage.from_array(v, dtype=v.dtype, backend="gt:mi355x", aligned_index=origin[k],
-                                  dimensions=tuple(axes[k])) for k, v in fields.items()}
+    axes, dd = fuzz_stencils.field_axes(seed), fuzz_stencils.data_dims(seed)
+    return {k: storage.from_array(v, dtype=np.dtype((v.dtype, dd[k])) if k in dd else v.dtype, backend="gt:mi355x",
+                                  aligned_index=origin[k], dimensions=tuple(axes[k])) for k, v in fields.items()}
 
 
 def _run_numpy(defn, seed):
