@@ -6,8 +6,9 @@ import fuzz_stencils
 # the default fuzz seeds (f64 programs: PARALLEL/FORWARD/BACKWARD, horizontal regions, staged
 # sweeps, sweep pairs and tile templates), the mixed-precision, K-offset,
 # lower-dimensional-field, operator,
-# while-loop / horizontal-region and mixed tile programs
-N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE = 160, 80, 60, 100, 100, 60
+# while-loop / horizontal-region, mixed tile and
+# gtscript-function programs
+N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE, N_FUNC = 160, 80, 60, 100, 100, 60, 60
 # programs the reference refuses: its upcaster raises "Type mismatch in `BinaryOp`. Types are
 # FLOAT32, INT64" on a comparison of sqrt(<int64>) (typed float32, as ours types it too) with an
 # int64; gt:mi355x accepts them. tests/test_fuzz.py still runs them against our
@@ -27,7 +28,8 @@ PINNED = list(range(60)) + list(range(1000, 1060)) + list(range(7000, 7024)) + l
     range(fuzz_stencils.LOWDIM_BASE, fuzz_stencils.LOWDIM_BASE + N_LOWDIM)) + list(
     range(fuzz_stencils.OPS_BASE, fuzz_stencils.OPS_BASE + N_OPS)) + list(
     range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + N_CTRL)) + list(
-    range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + N_TILE))
+    range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + N_TILE)) + list(
+    range(fuzz_stencils.FUNC_BASE, fuzz_stencils.FUNC_BASE + N_FUNC))
 PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED | REFERENCE_DIVERGENT]
 
 

@@ -118,13 +118,22 @@ TILE_BASE = 10000  # seeds >= TILE_BASE: mixed-precision tile programs with a ve
 TILE_FIELDS = {**MIXED_FIELDS, "v": "float64"}  # v: 2 data components per cell
 
 
+FUNC_BASE = 10100  # seeds >= FUNC_BASE: gtscript functions and a vector output (_generate_func)
+FUNC_FIELDS = {"a": "float64", "b": "float64", "c": "float32", "m": "int32", "out1": "float64", "out2": "float32",
+               "outv": "float64"}  # outv: 2 data components per cell
+
+
 def data_dims(seed):
     """{field: trailing data-dimension shape} of the fields that have data dimensions."""
+    if seed >= FUNC_BASE:
+        return {"outv": (2,)}
     return {"v": (2,)} if seed >= TILE_BASE else {}
 
 
 def field_dtypes(seed):
     """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= FUNC_BASE:
+        return dict(FUNC_FIELDS)
     if seed >= TILE_BASE:
         return dict(TILE_FIELDS)
     if seed >= OPS_BASE:
@@ -504,11 +513,70 @@ def _generate_tile(seed):
     return "\n".join(L) + "\n", name
 
 
+class _FuncGen(_MixedGen):
+    """Leaves over the f64/f32/int32 inputs of the function programs, and calls of the module's
+    gtscript functions (``self.funcs``: name -> arity) on field arguments."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if self.funcs and r.random() < 0.25:
+            fn, arity = r.choice(sorted(self.funcs.items()))
+            args = ", ".join(r.choice(("a", "b", "c", "m")) for _ in range(arity))
+            return f"{fn}({args})"
+        x = r.random()
+        if x < 0.1:
+            return repr(round(r.uniform(-3, 3), 3))
+        f = r.choice(("a", "b", "c", "m"))
+        return f"{f}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0]"
+
+
+def _generate_func(seed):
+    """Seeds >= FUNC_BASE: two or three @gtscript.function helpers (offset reads of their field
+    arguments, one calling another, one returning through an if/else), called from PARALLEL and
+    FORWARD computations, and a vector output written component by component."""
+    g = _FuncGen(seed)
+    g.funcs = {}
+    r = g.r
+    name = f"fuzz_{seed}"
+    L = []
+    L.append("@function")
+    L.append("def f0(x, y):")
+    L.append(f"    return (x[1, 0, 0] - y[0, 0, 0]) * {round(r.uniform(0.25, 2), 2)} + x[0, -1, 0]")
+    g.funcs["f0"] = 2
+    L.append("@function")
+    L.append("def f1(x):")
+    L.append(f"    return max(x[0, 1, 0], x[-1, 0, 0]) - f0(x, x) * 0.5")
+    g.funcs["f1"] = 1
+    if r.random() < 0.5:
+        L.append("@function")
+        L.append("def f2(x, y):")
+        L.append(f"    if x[0, 0, 0] > y[0, 0, 0]:")
+        L.append(f"        t = x[0, 0, 0] - y[1, 0, 0]")
+        L.append("    else:")
+        L.append(f"        t = y[0, 0, 0] * {round(r.uniform(0.5, 1.5), 2)}")
+        L.append("    return t")
+        g.funcs["f2"] = 2
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in FUNC_FIELDS.items() if n != "outv")
+    L.append(f"def {name}({sig}, outv: Field[(np.float64, (2,))], *, s: float):")
+    L.append("    with computation(PARALLEL), interval(...):")
+    L.append(f"        out1 = {g.expr(2, False, 'par')}")
+    L.append(f"        outv[0, 0, 0][0] = {g.expr(2, False, 'par')}")
+    L.append(f"        outv[0, 0, 0][1] = out1 * {g.expr(1, False, 'par')}")
+    L.append("    with computation(FORWARD):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            out2 = {g.expr(2, False, 'seq')}")
+    L.append("        with interval(1, None):")
+    L.append(f"            out2 = out2[0, 0, -1] * 0.5 + {g.expr(2, False, 'seq')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= FUNC_BASE:
+        return _generate_func(seed)
     if seed >= TILE_BASE:
         return _generate_tile(seed)
     if seed >= CTRL_BASE:

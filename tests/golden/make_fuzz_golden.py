@@ -32,7 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 HEADER = """import numpy as np
 from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
-from gt4py_amd.gtscript import (ceil, float32, float64, floor, int32, int64, isfinite, isnan, round,
+from gt4py_amd.gtscript import (ceil, float32, float64, floor, function, int32, int64, isfinite, isnan, round,
                                round_away_from_zero, sqrt, trunc)
 
 """
@@ -82,7 +82,7 @@ def main():
                 print(f"[refused] {seed}: {type(ex).__name__}: {str(ex).splitlines()[0][:120]}")
             else:
                 rec["outputs"] = {k: {"dtype": str(fields[k].dtype), "sha256": hashlib.sha256(fields[k].tobytes()).hexdigest()}
-                                  for k in ("out1", "out2")}
+                                  for k in sorted(fields) if k.startswith("out")}
             out[case_key(seed, deep)] = rec
     with open(os.path.join(HERE, "fuzz_reference.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)

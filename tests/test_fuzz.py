@@ -14,7 +14,7 @@ import fuzz_stencils
 
 HEADER = """import numpy as np
 from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
-from gt4py_amd.gtscript import (ceil, float32, float64, floor, int32, int64, isfinite, isnan, round,
+from gt4py_amd.gtscript import (ceil, float32, float64, floor, function, int32, int64, isfinite, isnan, round,
                                round_away_from_zero, sqrt, trunc)
 
 """
@@ -36,6 +36,8 @@ SEEDS += list(range(fuzz_stencils.OPS_BASE, fuzz_stencils.OPS_BASE + int(os.envi
 SEEDS += list(range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + int(os.environ.get("GTMI_FUZZ_CTRL", "100"))))
 # tile-kernel shape with mixed precision and a vector field
 SEEDS += list(range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + int(os.environ.get("GTMI_FUZZ_TILE", "60"))))
+# gtscript functions (nested calls, if/else inside) and a vector output written per component
+SEEDS += list(range(fuzz_stencils.FUNC_BASE, fuzz_stencils.FUNC_BASE + int(os.environ.get("GTMI_FUZZ_FUNC", "60"))))
 
 
 def _shape(seed):
@@ -122,6 +124,6 @@ def test_fuzz_program_matches_numpy(seed, tmp_path):
     ins, outs, origin = _inputs(seed)
     dev = to_device({**ins, **outs}, origin, seed)
     st(**dev, s=0.75, origin=origin, domain=_shape(seed))
-    for k in ("out1", "out2"):
+    for k in sorted(k for k in ref if k.startswith("out")):
         got = storage.to_numpy(dev[k])
         assert np.array_equal(got, ref[k]), f"seed {seed} field {k}:\n{src}"

@@ -21,7 +21,7 @@ from fuzz_pinned import CASES, case_key, case_shape
 HERE = os.path.dirname(os.path.abspath(__file__))
 HEADER = """import numpy as np
 from gt4py_amd.gtscript import BACKWARD, FORWARD, IJ, PARALLEL, Field, I, J, K, computation, horizontal, interval, region
-from gt4py_amd.gtscript import (ceil, float32, float64, floor, int32, int64, isfinite, isnan, round,
+from gt4py_amd.gtscript import (ceil, float32, float64, floor, function, int32, int64, isfinite, isnan, round,
                                round_away_from_zero, sqrt, trunc)
 
 """
