@@ -20,6 +20,7 @@ Literal precision follows ``literal_int_precision``/``literal_float_precision``
 from __future__ import annotations
 
 import ast
+import warnings
 import copy
 import dataclasses
 import builtins
@@ -847,6 +848,16 @@ class StencilParser:
         k_expr = None
         if isinstance(off[2], ir.Expr):
             k_expr, off[2] = off[2], 0
+            if off[0] or off[1]:
+                # as the reference: a run-time K offset becomes gtir.VariableKOffset(k=...) and the I/J
+                # offsets written beside it are dropped (frontend/defir_to_gtir.py:626-639,
+                # gtc/common.py:341-345 `to_dict` -> i = j = 0), so `f[1, 0, lev]` reads f[0, 0, lev]
+                warnings.warn(
+                    f"'{name}[{off[0]}, {off[1]}, <run-time K offset>]': the I/J offsets of a field read at a "
+                    f"run-time K offset are ignored, as in the reference (it reads '{name}' at the centre column)",
+                    stacklevel=2,
+                )
+                off[0] = off[1] = 0
         if any(isinstance(o, ir.Expr) for o in off[:2]):
             raise GTScriptSyntaxError(f"Run-time offsets are only supported along K ('{name}')")
         ndd = len(decl.data_dims) if decl is not None else 0

@@ -125,13 +125,20 @@ FUNC_FIELDS = {"a": "float64", "b": "float64", "c": "float32", "m": "int32", "ou
 
 def data_dims(seed):
     """{field: trailing data-dimension shape} of the fields that have data dimensions."""
+    if seed >= VK_BASE:
+        return {}
     if seed >= FUNC_BASE:
         return {"outv": (2,)}
     return {"v": (2,)} if seed >= TILE_BASE else {}
 
 
+VK_BASE = 10200  # seeds >= VK_BASE: run-time K offsets (_generate_vk), mixed precision
+
+
 def field_dtypes(seed):
     """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= VK_BASE:
+        return dict(MIXED_FIELDS)
     if seed >= FUNC_BASE:
         return dict(FUNC_FIELDS)
     if seed >= TILE_BASE:
@@ -570,11 +577,52 @@ def _generate_func(seed):
     return "\n".join(L) + "\n", name
 
 
+class _VkGen(_MixedGen):
+    """Mixed-precision leaves plus reads at a run-time K offset: ``(m[..] % 3) - 1`` in the middle
+    interval (levels k-1..k+1), ``m[..] % 2`` in a FORWARD sweep's interval(1, -1) (k..k+1)."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if kmode in ("vk3", "vk2") and r.random() < 0.35:
+            f = r.choice(("a", "b", "c"))
+            idx = f"m[{r.randint(-1, 1)}, {r.randint(-1, 1)}, 0]"
+            ko = f"({idx} % 3) - 1" if kmode == "vk3" else f"{idx} % 2"
+            return f"{f}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, {ko}]"
+        return super().leaf(allow_temps, "kwin" if kmode == "vk3" else "seq")
+
+
+def _generate_vk(seed):
+    """Seeds >= VK_BASE: fields read at run-time K offsets computed from an int32 field (the
+    column kernels' direct loads), in a PARALLEL computation and a FORWARD sweep."""
+    g = _VkGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    L.append("    with computation(PARALLEL):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            out1 = {g.expr(1, False, 'par')}")
+    L.append("        with interval(1, -1):")
+    L.append(f"            out1 = {g.expr(3, False, 'vk3')}")
+    L.append("        with interval(-1, None):")
+    L.append(f"            out1 = {g.expr(1, False, 'par')} * s")
+    L.append("    with computation(FORWARD):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            out2 = {g.expr(2, False, 'seq')}")
+    L.append("        with interval(1, -1):")
+    L.append(f"            out2 = out2[0, 0, -1] * 0.5 + {g.expr(2, False, 'vk2')}")
+    L.append("        with interval(-1, None):")
+    L.append(f"            out2 = out2[0, 0, -1] * 0.25 + {g.expr(1, False, 'seq')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= VK_BASE:
+        return _generate_vk(seed)
     if seed >= FUNC_BASE:
         return _generate_func(seed)
     if seed >= TILE_BASE:

@@ -1476,6 +1476,20 @@ case(
 )(variable_offsets_and_while_loop)
 
 
+def variable_k_offset_ij_dropped(in_field: F64, out_field: F64, idx: Field[np.int64]):
+    # the reference keeps only the K part of an offset whose K entry is an expression
+    # (defir_to_gtir.py:626-639): in_field[1, -1, expr] reads in_field[0, 0, expr]
+    with computation(PARALLEL), interval(1, -1):
+        out_field[0, 0, 0] = in_field[1, -1, (idx % 3) - 1] + in_field[0, 0, 0]
+
+
+case(
+    "variable_k_offset_ij_dropped",
+    fields={"in_field": fs(6, 5, 7), "out_field": fs(6, 5, 7, init="zeros"),
+            "idx": fs(6, 5, 7, dtype="i8", init=("int", -4, 5))},
+)(variable_k_offset_ij_dropped)
+
+
 def k_offset_scalar(in_field: F64, out_field: F64, scalar_value: int):
     with computation(PARALLEL), interval(1, None):
         out_field[0, 0, 0] = in_field[0, 0, scalar_value]

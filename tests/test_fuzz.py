@@ -38,6 +38,8 @@ SEEDS += list(range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + int(os.en
 SEEDS += list(range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + int(os.environ.get("GTMI_FUZZ_TILE", "60"))))
 # gtscript functions (nested calls, if/else inside) and a vector output written per component
 SEEDS += list(range(fuzz_stencils.FUNC_BASE, fuzz_stencils.FUNC_BASE + int(os.environ.get("GTMI_FUZZ_FUNC", "60"))))
+# run-time K offsets computed from an int32 field
+SEEDS += list(range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + int(os.environ.get("GTMI_FUZZ_VK", "60"))))
 
 
 def _shape(seed):
