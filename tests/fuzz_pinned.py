@@ -7,8 +7,9 @@ import fuzz_stencils
 # sweeps, sweep pairs and tile templates), the mixed-precision, K-offset,
 # lower-dimensional-field, operator,
 # while-loop / horizontal-region, mixed tile,
-# gtscript-function and run-time K offset programs
-N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE, N_FUNC, N_VK = 160, 80, 60, 100, 100, 60, 60, 60
+# gtscript-function, run-time K offset and
+# interval-partition programs
+N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE, N_FUNC, N_VK, N_IVL = 160, 80, 60, 100, 100, 60, 60, 60, 60
 # programs the reference refuses: its upcaster raises "Type mismatch in `BinaryOp`. Types are
 # FLOAT32, INT64" on a comparison of sqrt(<int64>) (typed float32, as ours types it too) with an
 # int64; gt:mi355x accepts them. tests/test_fuzz.py still runs them against our
@@ -30,7 +31,8 @@ PINNED = list(range(60)) + list(range(1000, 1060)) + list(range(7000, 7024)) + l
     range(fuzz_stencils.CTRL_BASE, fuzz_stencils.CTRL_BASE + N_CTRL)) + list(
     range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + N_TILE)) + list(
     range(fuzz_stencils.FUNC_BASE, fuzz_stencils.FUNC_BASE + N_FUNC)) + list(
-    range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + N_VK))
+    range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + N_VK)) + list(
+    range(fuzz_stencils.IVL_BASE, fuzz_stencils.IVL_BASE + N_IVL))
 PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED | REFERENCE_DIVERGENT]
 
 
@@ -40,7 +42,8 @@ PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED | REFERENCE_DIVERGENT]
 DEEP = [s for s in list(range(7000, 7024)) + list(range(fuzz_stencils.KOFF_BASE, fuzz_stencils.KOFF_BASE + N_KOFF))
         + list(range(fuzz_stencils.MIXED_BASE, fuzz_stencils.MIXED_BASE + 40))
         + list(range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + 30))
-        + list(range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + 30)) if s in PINNED]
+        + list(range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + 30))
+        + list(range(fuzz_stencils.IVL_BASE, fuzz_stencils.IVL_BASE + 30)) if s in PINNED]
 # golden record keys: "<seed>" at pinned_shape(seed), "<seed>@deep" at deep_shape(seed)
 CASES = [(s, False) for s in PINNED] + [(s, True) for s in DEEP]
 

@@ -133,6 +133,7 @@ def data_dims(seed):
 
 
 VK_BASE = 10200  # seeds >= VK_BASE: run-time K offsets (_generate_vk), mixed precision
+IVL_BASE = 10300  # seeds >= IVL_BASE: interval partitions with absolute/relative bounds and gaps
 
 
 def field_dtypes(seed):
@@ -616,11 +617,77 @@ def _generate_vk(seed):
     return "\n".join(L) + "\n", name
 
 
+class _IvlGen(_MixedGen):
+    """Mixed-precision leaves with K offsets restricted to the ones the current interval allows
+    (``self.kallowed``)."""
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if kmode == "ivl" and r.random() > 0.35:
+            f = r.choice(("a", "b", "c", "m"))
+            return f"{f}[{r.randint(-1, 1)}, {r.randint(-1, 1)}, {r.choice(self.kallowed)}]"
+        return super().leaf(allow_temps, "par")
+
+
+def _bounds(r):
+    """A random partition of the K axis as consecutive (lo, hi) bound pairs: absolute bounds from
+    the bottom, relative (negative) ones from the top, None = the end."""
+    cuts = sorted(r.sample([1, 2, 3, -3, -2, -1], r.randint(1, 4)), key=lambda b: (b < 0, b))
+    pts = [0] + cuts + [None]
+    return list(zip(pts[:-1], pts[1:]))
+
+
+def _generate_ivl(seed):
+    """Seeds >= IVL_BASE: a PARALLEL computation over a random partition of K into 2-5 intervals
+    (absolute and relative bounds, K offsets where the interval leaves room) and a FORWARD or
+    BACKWARD sweep over another partition with one interval left out (its levels keep the
+    output's previous values)."""
+    g = _IvlGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in MIXED_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+
+    def ivl(lo, hi):
+        return f"interval({lo}, {hi})"
+
+    def allowed(lo, hi):
+        return [0] + ([-1] if lo != 0 else []) + ([1] if hi is not None else [])
+
+    out = r.choice(("out1", "out2"))
+    L.append("    with computation(PARALLEL):")
+    for lo, hi in _bounds(r):
+        g.kallowed = allowed(lo, hi)
+        L.append(f"        with {ivl(lo, hi)}:")
+        L.append(f"            {out} = {g.expr(2, False, 'ivl')}")
+    other = "out2" if out == "out1" else "out1"
+    order = r.choice(("FORWARD", "BACKWARD"))
+    parts = _bounds(r)
+    if len(parts) > 2:
+        parts.pop(r.randrange(1, len(parts)))
+    if order == "BACKWARD":
+        parts = parts[::-1]
+    dk = -1 if order == "FORWARD" else 1
+    L.append(f"    with computation({order}):")
+    for q, (lo, hi) in enumerate(parts):
+        g.kallowed = allowed(lo, hi)
+        L.append(f"        with {ivl(lo, hi)}:")
+        # the neighbour level the sweep came from exists when this is not the sweep's first level
+        carried = (lo != 0) if order == "FORWARD" else (hi is not None)
+        if carried:
+            L.append(f"            {other} = {other}[0, 0, {dk}] * 0.5 + {g.expr(2, False, 'ivl')}")
+        else:
+            L.append(f"            {other} = {g.expr(2, False, 'ivl')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= IVL_BASE:
+        return _generate_ivl(seed)
     if seed >= VK_BASE:
         return _generate_vk(seed)
     if seed >= FUNC_BASE:
