@@ -7,9 +7,9 @@ import fuzz_stencils
 # sweeps, sweep pairs and tile templates), the mixed-precision, K-offset,
 # lower-dimensional-field, operator,
 # while-loop / horizontal-region, mixed tile,
-# gtscript-function, run-time K offset and
-# interval-partition programs
-N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE, N_FUNC, N_VK, N_IVL = 160, 80, 60, 100, 100, 60, 60, 60, 60
+# gtscript-function, run-time K offset,
+# interval-partition and absolute-K programs
+N_MIXED, N_KOFF, N_LOWDIM, N_OPS, N_CTRL, N_TILE, N_FUNC, N_VK, N_IVL, N_ABSK = 160, 80, 60, 100, 100, 60, 60, 60, 60, 40
 # programs the reference refuses: its upcaster raises "Type mismatch in `BinaryOp`. Types are
 # FLOAT32, INT64" on a comparison of sqrt(<int64>) (typed float32, as ours types it too) with an
 # int64; gt:mi355x accepts them. tests/test_fuzz.py still runs them against our
@@ -32,7 +32,8 @@ PINNED = list(range(60)) + list(range(1000, 1060)) + list(range(7000, 7024)) + l
     range(fuzz_stencils.TILE_BASE, fuzz_stencils.TILE_BASE + N_TILE)) + list(
     range(fuzz_stencils.FUNC_BASE, fuzz_stencils.FUNC_BASE + N_FUNC)) + list(
     range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + N_VK)) + list(
-    range(fuzz_stencils.IVL_BASE, fuzz_stencils.IVL_BASE + N_IVL))
+    range(fuzz_stencils.IVL_BASE, fuzz_stencils.IVL_BASE + N_IVL)) + list(
+    range(fuzz_stencils.ABSK_BASE, fuzz_stencils.ABSK_BASE + N_ABSK))
 PINNED = [s for s in PINNED if s not in REFERENCE_REFUSED | REFERENCE_DIVERGENT]
 
 

@@ -134,10 +134,14 @@ def data_dims(seed):
 
 VK_BASE = 10200  # seeds >= VK_BASE: run-time K offsets (_generate_vk), mixed precision
 IVL_BASE = 10300  # seeds >= IVL_BASE: interval partitions with absolute/relative bounds and gaps
+ABSK_BASE = 10400  # seeds >= ABSK_BASE: absolute K indexing (_generate_absk), f64 (debug-backend oracle)
+ABSK_FIELDS = {"a": "float64", "b": "float64", "c": "float64", "m": "int32", "out1": "float64", "out2": "float64"}
 
 
 def field_dtypes(seed):
     """{field: numpy dtype name} of the program ``generate(seed)`` writes."""
+    if seed >= ABSK_BASE:
+        return dict(ABSK_FIELDS)
     if seed >= VK_BASE:
         return dict(MIXED_FIELDS)
     if seed >= FUNC_BASE:
@@ -681,11 +685,60 @@ def _generate_ivl(seed):
     return "\n".join(L) + "\n", name
 
 
+class _AbskGen(_MixedGen):
+    """f64 leaves plus ``.at(K=...)`` reads at a constant level or at a level computed from m. No
+    ternaries: the reference's debug backend (the oracle here) prints a ternary without parentheses
+    (gtc/debug/debug_codegen.py:358-359), so `(x if c else y) - z` runs as `x if c else (y - z)`."""
+
+    def expr(self, depth, allow_temps, kmode):
+        r = self.r
+        if depth == 0 or r.random() < 0.25:
+            return self.leaf(allow_temps, kmode)
+        x, y = self.expr(depth - 1, allow_temps, kmode), self.expr(depth - 1, allow_temps, kmode)
+        k = r.random()
+        if k < 0.6:
+            return f"({x} {r.choice(('+', '-', '*'))} {y})"
+        if k < 0.7:
+            return f"({x} / (abs({y}) + 1.5))"
+        if k < 0.9:
+            return f"{r.choice(('min', 'max'))}({x}, {y})"
+        return f"abs({x})"
+
+    def leaf(self, allow_temps, kmode):
+        r = self.r
+        if r.random() < 0.3:
+            f = r.choice(("a", "b", "c"))
+            lev = r.choice((str(r.randint(0, 5)), f"(m[0, 0, 0] % 3) + {r.randint(0, 3)}"))
+            return f"{f}.at(K={lev})"
+        return super().leaf(allow_temps, kmode)
+
+
+def _generate_absk(seed):
+    """Seeds >= ABSK_BASE: reads at absolute levels (``field.at(K=...)``, constant or from an int32
+    field) beside relative reads, in a PARALLEL computation and a FORWARD sweep; f64 fields so the
+    reference's debug backend (its only backend for absolute K indexing) is an exact oracle."""
+    g = _AbskGen(seed)
+    r = g.r
+    name = f"fuzz_{seed}"
+    sig = ", ".join(f"{n}: Field[np.{t}]" for n, t in ABSK_FIELDS.items())
+    L = [f"def {name}({sig}, *, s: float):"]
+    L.append("    with computation(PARALLEL), interval(...):")
+    L.append(f"        out1 = {g.expr(3, False, 'par')}")
+    L.append("    with computation(FORWARD):")
+    L.append("        with interval(0, 1):")
+    L.append(f"            out2 = {g.expr(2, False, 'seq')}")
+    L.append("        with interval(1, None):")
+    L.append(f"            out2 = out2[0, 0, -1] * 0.5 + {g.expr(2, False, 'seq')}")
+    return "\n".join(L) + "\n", name
+
+
 def generate(seed):
     """Return (source, function name) of a random stencil; seeds >= 1000 add horizontal regions,
     cross-computation temporaries read at IJ offsets and sweeps needing the staged lowering;
     seeds >= 7000 are the sweep-pair and tile templates of ``_generate_v3``; seeds >=
     ``MIXED_BASE`` the mixed-precision programs of ``_generate_mixed``."""
+    if seed >= ABSK_BASE:
+        return _generate_absk(seed)
     if seed >= IVL_BASE:
         return _generate_ivl(seed)
     if seed >= VK_BASE:

@@ -74,7 +74,12 @@ def main():
             rec = {"source_sha256": hashlib.sha256(src.encode()).hexdigest(), "shape": list(shape)}
             try:
                 defn = _load(src, name, tmp, seed)
-                st = ref_gtscript.stencil(backend="numpy", definition=defn, name=f"fuzzref.s{seed}", rebuild=False)
+                # absolute K indexing: the reference's numpy backend raises for it, its debug backend
+                # is the oracle (as for the golden fixtures, tests/golden/make_golden.py)
+                backend = "debug" if seed >= fs.ABSK_BASE else "numpy"
+                if backend != "numpy":
+                    rec["backend"] = backend
+                st = ref_gtscript.stencil(backend=backend, definition=defn, name=f"fuzzref.s{seed}", rebuild=False)
                 fields, origin = fs.make_inputs(seed, shape)
                 st(**fields, s=0.75, origin=origin, domain=shape)
             except Exception as ex:  # the reference refuses the program: record it

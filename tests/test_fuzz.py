@@ -42,6 +42,8 @@ SEEDS += list(range(fuzz_stencils.FUNC_BASE, fuzz_stencils.FUNC_BASE + int(os.en
 SEEDS += list(range(fuzz_stencils.VK_BASE, fuzz_stencils.VK_BASE + int(os.environ.get("GTMI_FUZZ_VK", "60"))))
 # K partitions with absolute/relative interval bounds and gaps
 SEEDS += list(range(fuzz_stencils.IVL_BASE, fuzz_stencils.IVL_BASE + int(os.environ.get("GTMI_FUZZ_IVL", "60"))))
+# absolute K indexing (field.at(K=...)), f64
+SEEDS += list(range(fuzz_stencils.ABSK_BASE, fuzz_stencils.ABSK_BASE + int(os.environ.get("GTMI_FUZZ_ABSK", "40"))))
 
 
 def _shape(seed):
@@ -51,7 +53,7 @@ def _shape(seed):
     nk = int(os.environ.get("GTMI_FUZZ_NK", "0"))
     ni, nj, nk0 = (13, 11, 8) if seed % 2 == 0 else (300, 45, 6)
     if seed >= fuzz_stencils.IVL_BASE:
-        nk0 = 8  # interval bounds up to 3 and -3: at least 7 levels
+        nk0 = 8  # interval bounds up to 3 and -3 / absolute levels up to 5: at least 7 levels
     return ni, nj, nk or nk0
 
 
